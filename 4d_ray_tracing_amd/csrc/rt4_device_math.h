@@ -1,0 +1,148 @@
+// rt4_device_math.h — fp32 building blocks of the trace kernel (gfx950).
+//
+// Numerical contract: the GLSL built-ins of executable/shader.frag are given ONE
+// definition here, evaluated with explicit v_fma_f32 where the contract says fma and separately
+// rounded ops everywhere else. The build uses -ffp-contract=off (no silent fusion) and correctly
+// rounded fp32 division/sqrt, so every value is reproducible bit for bit on the host.
+//   dot(a,b) = fma(a.w,b.w, fma(a.z,b.z, fma(a.y,b.y, a.x*b.x)))
+//   vector multiply-add forms of the shader are one fma per component.
+//   acos/asin: Cephes asinf kernel; sin/cos: pi/2 Cody-Waite reduction + Cephes kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rt4 {
+
+constexpr float PI_F = 3.14159265f;   // shader.frag:23
+constexpr float SMALL_F = 0.0003f;    // shader.frag:24
+constexpr float PIO2_F = 1.57079637050628662109375f;
+constexpr float PIO2_LO = -4.37113900018624283e-8f;
+constexpr float TWO_OVER_PI = 0.636619772367581343f;
+constexpr int NEWTON_CAP = 64;
+
+struct V4 { float x, y, z, w; };
+struct V3 { float x, y, z; };
+
+__device__ __forceinline__ float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+__device__ __forceinline__ V4 make4(float x, float y, float z, float w) { return V4{x, y, z, w}; }
+__device__ __forceinline__ V4 ld4(const float* p) { return V4{p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ V4 add(V4 a, V4 b) { return V4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+__device__ __forceinline__ V4 sub(V4 a, V4 b) { return V4{a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; }
+__device__ __forceinline__ V4 mul(V4 a, float s) { return V4{a.x * s, a.y * s, a.z * s, a.w * s}; }
+__device__ __forceinline__ V4 divs(V4 a, float s) { return V4{a.x / s, a.y / s, a.z / s, a.w / s}; }
+__device__ __forceinline__ V4 neg(V4 a) { return V4{-a.x, -a.y, -a.z, -a.w}; }
+__device__ __forceinline__ V4 mad(V4 a, float s, V4 c) {  // a*s + c
+  return V4{fmaf_(a.x, s, c.x), fmaf_(a.y, s, c.y), fmaf_(a.z, s, c.z), fmaf_(a.w, s, c.w)};
+}
+__device__ __forceinline__ float dot(V4 a, V4 b) {
+  return fmaf_(a.w, b.w, fmaf_(a.z, b.z, fmaf_(a.y, b.y, a.x * b.x)));
+}
+__device__ __forceinline__ float length(V4 v) { return __builtin_sqrtf(dot(v, v)); }
+
+// ---- transcendentals ------------------------------------------------------------------------
+__device__ __forceinline__ float asin_core(float s, float z) {
+  float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
+                        7.4953002686e-2f), z, 1.6666752422e-1f);
+  return fmaf_(p, z * s, s);
+}
+
+// Branch-free form of the oracle's rt4m_asin: both arms compute the same op sequence per lane.
+__device__ __forceinline__ float asin_(float x) {
+  float a = __builtin_fabsf(x);
+  bool big = a > 0.5f;
+  float zb = 0.5f * (1.0f - a);
+  float z = big ? zb : a * a;
+  float s = big ? __builtin_sqrtf(zb) : a;
+  float c = asin_core(s, z);
+  float r = big ? (PIO2_F - 2.0f * c) : c;
+  return __builtin_copysignf(r, x);
+}
+
+__device__ __forceinline__ float acos_(float x) {
+  float a = __builtin_fabsf(x);
+  bool big = a > 0.5f;
+  float zb = 0.5f * (1.0f - a);
+  float z = big ? zb : x * x;
+  float s = big ? __builtin_sqrtf(zb) : x;
+  float c = asin_core(s, z);
+  float t = 2.0f * c;
+  float rb = x > 0.0f ? t : PI_F - t;
+  return big ? rb : PIO2_F - c;
+}
+
+__device__ __forceinline__ float sin_kernel(float r) {
+  float z = r * r;
+  float p = fmaf_(fmaf_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  return fmaf_(p, z * r, r);
+}
+__device__ __forceinline__ float cos_kernel(float r) {
+  float z = r * r;
+  float p = fmaf_(fmaf_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+  return fmaf_(p, z * z, fmaf_(-0.5f, z, 1.0f));
+}
+__device__ __forceinline__ void reduce_pio2(float x, float& r, int& q) {
+  float j = __builtin_rintf(x * TWO_OVER_PI);
+  r = fmaf_(-j, PIO2_F, x);
+  r = fmaf_(-j, PIO2_LO, r);
+  q = (__builtin_fabsf(j) < 8388608.0f) ? (static_cast<int>(j) & 3) : 0;
+}
+__device__ __forceinline__ float sin_(float x) {
+  float r; int q; reduce_pio2(x, r, q);
+  float s = sin_kernel(r), c = cos_kernel(r);
+  float v = (q & 1) ? c : s;
+  return (q & 2) ? -v : v;
+}
+__device__ __forceinline__ float cos_(float x) {
+  float r; int q; reduce_pio2(x, r, q);
+  float s = sin_kernel(r), c = cos_kernel(r);
+  float v = (q & 1) ? s : c;
+  return ((q + 1) & 2) ? -v : v;
+}
+// sin and cos of the same angle share the reduction and both kernels (rand_drct, shader.frag:129).
+__device__ __forceinline__ void sincos_(float x, float& sv, float& cv) {
+  float r; int q; reduce_pio2(x, r, q);
+  float s = sin_kernel(r), c = cos_kernel(r);
+  float vs = (q & 1) ? c : s;
+  float vc = (q & 1) ? s : c;
+  sv = (q & 2) ? -vs : vs;
+  cv = ((q + 1) & 2) ? -vc : vc;
+}
+
+// ---- RNG (shader.frag:90-121) -----------------------------------------------------------------
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {  // :94-102
+  x += (x << 10);
+  x ^= (x >> 6);
+  x += (x << 3);
+  x ^= (x >> 11);
+  x += (x << 15);
+  x ^= (x >> 9);
+  return x;
+}
+
+// ---- S^3 sampler (shader.frag:136-150) ------------------------------------------------------------
+__device__ __forceinline__ float volume_by_w(float w) {  // :136-138
+  return (w * __builtin_sqrtf(1.0f - w * w) - acos_(w)) / PI_F + 1.0f;
+}
+__device__ __forceinline__ float w_by_volume(float v, int* iters) {  // :141-150
+  float old_w;
+  float new_w = 0.0f;
+  int it = 0;
+  do {
+    old_w = new_w;
+    float old_v = volume_by_w(old_w);
+    // one volume_by_w per iteration for the finite difference: both arms of the shader's ternary
+    // evaluate volume_by_w(old_w -/+ SMALL), so the selected argument is computed first.
+    bool pos = old_w > 0.0f;
+    float probe = volume_by_w(pos ? old_w - SMALL_F : old_w + SMALL_F);
+    float df = pos ? old_v - probe : probe - old_v;
+    new_w = old_w - SMALL_F / df * (old_v - v);
+    ++it;
+  } while (__builtin_fabsf(new_w - old_w) >= SMALL_F && it < NEWTON_CAP);
+  if (iters) *iters = it;
+  return new_w;
+}
+
+}  // namespace rt4

@@ -1,0 +1,294 @@
+/*
+ * rt4.h — C ABI of the MI355X-native 4D path tracer (the drop-in boundary).
+ *
+ * The reference (BusyginIvan/4D_ray_tracing) has exactly one hot path: the per-cell trace loop of
+ * executable/shader.frag (GLSL 330), driven by SFML through uniforms and one draw call per window.
+ * This header replaces that boundary with plain C: POD structs, pointers and sizes, int status codes.
+ *
+ * Reference interface each entry point replaces (paths relative to the reference root):
+ *   rt4_uniforms                  <- the 13 GLSL uniforms, executable/shader.frag:5-19, set through
+ *                                    sf::Shader::setUniform in src/main.cpp:28-38,86-91 and
+ *                                    src/windows/windows.cpp:41-44
+ *   rt4_scene_desc                <- the scene block pasted into shader.frag (shader.frag:412-451,
+ *                                    scenes/<name>.frag) + optional final_light override (shader.frag:454-468)
+ *   rt4_scene_load_frag/parse     <- "paste a scene over shader.frag" workflow (executable/README.md:9-11),
+ *                                    compiled at run time by sf::Shader::loadFromFile (src/main.cpp:26)
+ *   rt4_properties_*              <- Properties (inc/properties.h:8-18, src/properties.cpp:12-77)
+ *   rt4_orientation_update        <- Orientation::update (src/controls.cpp:72-86)
+ *   rt4_uniforms_from_properties  <- initShader + first-frame uniforms (src/main.cpp:25-39,86-91),
+ *                                    initControls (src/controls.cpp:140-159), CellsWindow
+ *                                    (src/windows/windows.cpp:6-13,24-34)
+ *   rt4_section_basis             <- ThreeWindowGroup::drawShaderImage (three_window_group.cpp:42-46)
+ *   rt4_render_device / _host     <- CellsWindow::drawShaderImage -> texture.draw(sprite,&shader)
+ *                                    (src/windows/windows.cpp:40-47): the "kernel launch"
+ *
+ * Conventions
+ *   - Status: 0 = RT4_OK, negative = error; `err` (may be NULL) receives a NUL-terminated message.
+ *     Nothing in the library aborts (the reference's error() aborts: src/util/util.cpp:9-12).
+ *   - Images are float RGBA (16 B per pixel). Row 0 is the TOP of the displayed image, which in the
+ *     reference is gl_FragCoord.y = 0.5 (RenderTexture::display() is never called).
+ *   - The framebuffer is read (old_frame) and written in place by the lane that owns the pixel.
+ *   - Re-entrant per (context, stream). One context per device per host thread.
+ */
+#ifndef RT4_H
+#define RT4_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT4_ABI_VERSION 1
+
+enum rt4_status {
+  RT4_OK = 0,
+  RT4_ERR_ARG = -1,      /* bad argument / out-of-range value */
+  RT4_ERR_IO = -2,       /* file cannot be opened or read */
+  RT4_ERR_PARSE = -3,    /* properties or scene text not understood */
+  RT4_ERR_HIP = -4,      /* HIP runtime error (no device, launch failure, ...) */
+  RT4_ERR_CAPACITY = -5, /* scene exceeds the RT4_MAX_* limits below */
+  RT4_ERR_PROPERTY = -6  /* missing key / bad value (reference: Properties::get* error paths) */
+};
+
+/* ---- uniforms: executable/shader.frag:5-19 (field-for-field) ------------------------------- */
+typedef struct rt4_uniforms {
+  int32_t seed;               /* shader.frag:5   (main.cpp:86, time based there; fixed here)    */
+  int32_t samples;            /* shader.frag:6   ray_tracing.samples                          */
+  int32_t reflections_amount; /* shader.frag:7   ray_tracing.reflections_amount               */
+  float small_indent;         /* shader.frag:8   ray_tracing.small_indent                     */
+  float resolution[2];        /* shader.frag:10  cells (windows.cpp:41)                       */
+  float part;                 /* shader.frag:12  1/frameNumber (main.cpp:87)                  */
+  float light_to_color_conversion_coefficient; /* shader.frag:13                            */
+  float mtr_sizes[2];         /* shader.frag:16  (matrix_height*GOLDEN, matrix_height)        */
+  float focus[4];             /* shader.frag:17                                               */
+  float vec_to_mtr[4];        /* shader.frag:18  forward * focus_to_matrix_distance           */
+  float top_drct[4];          /* shader.frag:19                                               */
+  float right_drct[4];        /* shader.frag:19                                               */
+} rt4_uniforms;
+
+/* ---- scene: the primitive types of shader.frag:163-400 --------------------------------------- */
+typedef struct rt4_material { /* shader.frag:163-167 */
+  float glow;
+  float refl_prob;
+  float color[3];
+} rt4_material;
+
+typedef struct rt4_space { /* visible_space, shader.frag:225-228 */
+  float point[4];
+  float norm[4];
+  rt4_material material;
+} rt4_space;
+
+typedef struct rt4_sphere { /* visible_sphere, shader.frag:189-192 */
+  float center[4];
+  float r;
+  rt4_material material;
+} rt4_sphere;
+
+typedef struct rt4_cylinder { /* visible_cylinder, shader.frag:243-247 */
+  float point[4];
+  float axis1[4];
+  float axis2[4];
+  float r;
+  rt4_material material;
+} rt4_cylinder;
+
+typedef struct rt4_cylinders_union { /* visible_cylinders_union, shader.frag:279-281 */
+  rt4_cylinder cylinder1, cylinder2;
+} rt4_cylinders_union;
+
+typedef struct rt4_tiger { /* visible_tiger, shader.frag:298-300 (built by init_tiger :303-314) */
+  rt4_cylinder inner_cyl1, outer_cyl1, inner_cyl2, outer_cyl2;
+} rt4_tiger;
+
+typedef struct rt4_cube { /* visible_cube, shader.frag:345-350 */
+  float point[4]; /* space.point */
+  float norm[4];  /* space.norm  */
+  float x[4], y[4], z[4];
+  float r;
+  rt4_material material;
+} rt4_cube;
+
+typedef struct rt4_hypercube { /* visible_hypercube, shader.frag:370-372 (init_hypercube :374-392) */
+  rt4_cube cubes[8];
+} rt4_hypercube;
+
+typedef struct rt4_sun { /* sun_properties, shader.frag:404-409 */
+  float drct[4];
+  float angular_size;
+  float light[3];
+  float sharpness;
+} rt4_sun;
+
+/* One statement `inter = closest(<group>_intersection(...), inter);` of find_intersection
+ * (shader.frag:434-451). Groups are tested in array order; ties keep the accumulated hit. */
+enum rt4_group_kind {
+  RT4_GROUP_SPACES = 1,           /* for (i) space_intersection(spaces[i], ray)            :437-438 */
+  RT4_GROUP_SPHERES = 2,          /* for (i) sphere_intersection(spheres[i], ray, outer)   :440-441 */
+  RT4_GROUP_CYLINDERS = 3,        /* for (i) cylinder_intersection(cylinders[i], ray, outer) :443-444 */
+  RT4_GROUP_CYLINDERS_UNION = 4,  /* cylinders_union_intersection(u, ray)                   :446 */
+  RT4_GROUP_HYPERCUBE = 5,        /* hypercube_intersection(h, ray)                         :447 */
+  RT4_GROUP_TIGER = 6             /* tiger_intersection(t, ray)                             :448 */
+};
+
+typedef struct rt4_group {
+  int32_t kind;      /* rt4_group_kind */
+  int32_t first;     /* index of the first object in the kind's array */
+  int32_t count;     /* objects tested by this statement (1 for union/hypercube/tiger) */
+  int32_t outer;     /* `outer` argument of sphere/cylinder tests (shader.frag:197,251) */
+  int32_t new_first; /* 1: closest(new, inter) (reference form: tie keeps inter);
+                        0: closest(inter, new) (tie takes the new hit) */
+} rt4_group;
+
+#define RT4_MAX_GROUPS 16
+#define RT4_MAX_SPACES 32
+#define RT4_MAX_SPHERES 32
+#define RT4_MAX_CYLINDERS 16
+#define RT4_MAX_UNIONS 4
+#define RT4_MAX_HYPERCUBES 4
+#define RT4_MAX_TIGERS 4
+
+enum rt4_final_light_mode {
+  RT4_FINAL_LIGHT_SUN_SKY = 0, /* default final_light, shader.frag:454-468 */
+  RT4_FINAL_LIGHT_CONSTANT = 1 /* override returning a constant vec3 (S-room: scenes/Комната...:38-40) */
+};
+
+typedef struct rt4_scene_desc {
+  float sky_light[3];         /* shader.frag:414 */
+  rt4_sun sun;                /* shader.frag:415 */
+  int32_t final_light_mode;   /* rt4_final_light_mode */
+  float final_light_const[3]; /* value returned by a constant override */
+  int32_t n_groups;
+  rt4_group groups[RT4_MAX_GROUPS];
+  int32_t n_spaces;
+  rt4_space spaces[RT4_MAX_SPACES];
+  int32_t n_spheres;
+  rt4_sphere spheres[RT4_MAX_SPHERES];
+  int32_t n_cylinders;
+  rt4_cylinder cylinders[RT4_MAX_CYLINDERS];
+  int32_t n_unions;
+  rt4_cylinders_union unions[RT4_MAX_UNIONS];
+  int32_t n_hypercubes;
+  rt4_hypercube hypercubes[RT4_MAX_HYPERCUBES];
+  int32_t n_tigers;
+  rt4_tiger tigers[RT4_MAX_TIGERS];
+} rt4_scene_desc;
+
+/* ---- library info ------------------------------------------------------------------------- */
+int rt4_abi_version(void);
+const char* rt4_build_info(void); /* "rt4 <ver> gfx950 hip <ver> ..." */
+size_t rt4_scene_desc_size(void); /* sizeof(rt4_scene_desc), for binding-layout checks */
+size_t rt4_uniforms_size(void);
+
+/* ---- properties.txt (src/properties.cpp:12-77) --------------------------------------------- */
+typedef struct rt4_properties rt4_properties;
+int rt4_properties_load(const char* path, rt4_properties** out, char* err, size_t errlen);
+int rt4_properties_parse(const char* text, size_t len, rt4_properties** out, char* err, size_t errlen);
+void rt4_properties_free(rt4_properties* p);
+int rt4_properties_has(const rt4_properties* p, const char* key);
+/* getString: copies the value (truncated to buflen-1); *needed receives strlen(value) if non-NULL */
+int rt4_properties_get_string(const rt4_properties* p, const char* key, char* buf, size_t buflen,
+                              size_t* needed, char* err, size_t errlen);
+int rt4_properties_get_int(const rt4_properties* p, const char* key, int32_t* out, char* err, size_t errlen);
+int rt4_properties_get_uint(const rt4_properties* p, const char* key, uint32_t* out, char* err, size_t errlen);
+int rt4_properties_get_float(const rt4_properties* p, const char* key, float* out, char* err, size_t errlen);
+int rt4_properties_get_bool(const rt4_properties* p, const char* key, int* out, char* err, size_t errlen);
+
+/* ---- camera (src/controls.cpp:64-86) ------------------------------------------------------- */
+typedef struct rt4_orientation {
+  float forward[4], top[4], right[4], w_drct[4];
+  float horizontal_forward[4], horizontal_right[4], vertical_top[4];
+} rt4_orientation;
+/* angles in radians (the reference converts degrees with convertDegreesToRadians, math.cpp:29) */
+void rt4_orientation_update(float fi, float te, float psi, rt4_orientation* out);
+
+enum rt4_section { /* three_window_group.cpp:42-46 */
+  RT4_SECTION_YXZ = 0, /* main window:  top_drct = top,    right_drct = right */
+  RT4_SECTION_YWZ = 1, /* extra window: top_drct = top,    right_drct = w     */
+  RT4_SECTION_YXW = 2  /* extra window: top_drct = w,      right_drct = right */
+};
+int rt4_section_basis(const rt4_orientation* o, int section, float top[4], float right[4]);
+
+/* Builds every uniform the reference host sets for the first frame of a still camera:
+ * samples/reflections/indent/k/mtr_sizes (main.cpp:28-38), focus + vec_to_mtr (main.cpp:88-91,
+ * controls.cpp:151-158), top/right for `section` and resolution = cells (windows.cpp:41-44),
+ * part = 1 (frameNumber 1), seed = 0. cells_w/cells_h are the render resolution. */
+int rt4_uniforms_from_properties(const rt4_properties* p, int32_t cells_w, int32_t cells_h, int section,
+                                 rt4_uniforms* out, rt4_orientation* orientation_out, char* err,
+                                 size_t errlen);
+/* cells of a window: width/cell_size, (width/GOLDEN)/cell_size (windows.cpp:6-13,25-26);
+ * window_type is "main" or "additional" (keys window.<type>.width / .cell_size). */
+int rt4_window_cells(const rt4_properties* p, const char* window_type, int32_t* cells_w, int32_t* cells_h,
+                     char* err, size_t errlen);
+
+/* ---- scenes ------------------------------------------------------------------------------- */
+/* Accepts a scene snippet (scenes/<name>.frag) or a whole shader.frag; UTF-8 paths. */
+int rt4_scene_load_frag(const char* path, rt4_scene_desc* out, char* err, size_t errlen);
+int rt4_scene_parse_frag(const char* text, size_t len, rt4_scene_desc* out, char* err, size_t errlen);
+int rt4_scene_validate(const rt4_scene_desc* s, char* err, size_t errlen);
+/* The reference's five scenes, rebuilt from their values (scenes/<name>.frag, executable/shader.frag):
+ * "sphere" (Шар, плоскость и светилник), "room" (Комната со сферой), "tiger" (Фигура tiger; also
+ * the shipped shader.frag default), "cylinder4d" (Четырёхмерный цилиндр), "hypercube" (Гиперкуб). */
+int rt4_scene_builtin(const char* name, rt4_scene_desc* out, char* err, size_t errlen);
+
+/* ---- device context + trace kernel --------------------------------------------------------- */
+typedef struct rt4_context rt4_context;
+
+/* Memoise w_by_volume (shader.frag:141-150) over its whole input domain: rand() yields only
+ * 2^23 values (shader.frag:111-118), so a 32 MiB table built on the device at context creation
+ * by the same device function reproduces every Newton result bit for bit. */
+#define RT4_FLAG_SAMPLER_LUT 0x1u
+
+int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err, size_t errlen);
+int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* err, size_t errlen);
+void rt4_context_destroy(rt4_context* ctx);
+
+/* Pixel set of one launch. Local row i in [0,h) maps to image row
+ *   band_rows == 0 : y0 + i
+ *   band_rows  > 0 : y0 + (i / band_rows) * band_step + (i % band_rows)
+ * and local column j in [0,w) to image column x0 + j. Scene coordinates come from the full image
+ * size in uniforms.resolution, so any partition renders exactly the pixels of the whole image. */
+typedef struct rt4_region {
+  int32_t x0, y0, w, h;
+  int32_t band_rows;
+  int32_t band_step;
+} rt4_region;
+
+/* d_rgba: device float4 framebuffer; pixel (i, j) at d_rgba + 4*(i*row_stride_px + j).
+ * Holds old_frame on entry and mix(old, new, part) on return (shader.frag:524-527).
+ * d_counter (may be NULL): device uint64 incremented by the number of find_intersection calls
+ * (one per ray-bounce, shader.frag:475). stream: hipStream_t (NULL = default stream).
+ * Asynchronous: no host synchronisation, no allocation (graph-capture safe). */
+int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
+                      int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err,
+                      size_t errlen);
+
+/* Host-buffer convenience wrapper: copies rgba (same layout) to the device, renders, copies back,
+ * synchronises. n_intersections (may be NULL) receives the count. */
+int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* rgba,
+                    int64_t row_stride_px, uint64_t* n_intersections, char* err, size_t errlen);
+
+/* ---- diagnostics (used by the parity tests; not on the render path) ------------------------- */
+enum rt4_eval_fn {
+  RT4_EVAL_ACOS = 0, RT4_EVAL_ASIN = 1, RT4_EVAL_SIN = 2, RT4_EVAL_COS = 3,
+  RT4_EVAL_VOLUME_BY_W = 4, /* shader.frag:136-138 */
+  RT4_EVAL_W_BY_VOLUME = 5, /* shader.frag:141-150; aux[i] = Newton iterations */
+  RT4_EVAL_HASH = 6         /* shader.frag:94-102 on the bit pattern of in[i] */
+};
+/* Evaluates a device math function element-wise (synchronous; host buffers). */
+int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_t* aux, int64_t n, char* err,
+                   size_t errlen);
+
+/* Runs find_intersection (shader.frag:434-451) for n rays of the context's scene on the device.
+ * rays: n x 8 floats (point xyzw, drct xyzw). out: n x 8 floats {hit(0/1), dist, norm xyzw,
+ * glow, refl_prob}; out_color: n x 3 floats. Synchronous; host buffers. */
+int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out, float* out_color, int64_t n,
+                                char* err, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT4_H */

@@ -1,0 +1,47 @@
+import importlib
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+REFERENCE = "/root/reference"  # present only in the build container, never on the GPU box
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box via gpurun)")
+    config.addinivalue_line("markers", "slow: long CPU test")
+
+
+@pytest.fixture(scope="session")
+def rt4():
+    return importlib.import_module("4d_ray_tracing_amd")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle_lib
+
+    oracle_lib.lib()
+    return oracle_lib
+
+
+@pytest.fixture(scope="session")
+def tracer(rt4):
+    t = rt4.Tracer(device=0)
+    yield t
+    t.close()
+
+
+@pytest.fixture(scope="session")
+def tracer_lut(rt4):
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT)
+    yield t
+    t.close()
+
+
+def reference_available():
+    return os.path.isdir(os.path.join(REFERENCE, "scenes"))

@@ -1,0 +1,88 @@
+"""ctypes loader of the CPU oracle (oracle/build/librt4_oracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module, and only as
+the checker / CPU baseline; the product (librt4.so) never loads it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_PATH = os.path.join(ROOT, "oracle", "build", "librt4_oracle.so")
+
+
+def load():
+    if not os.path.exists(ORACLE_PATH):
+        raise FileNotFoundError(f"oracle not built: {ORACLE_PATH} (make -C oracle)")
+    lib = ctypes.CDLL(ORACLE_PATH)
+    lib.oracle_hash.argtypes = [c_uint32]
+    lib.oracle_hash.restype = c_uint32
+    lib.oracle_scene_desc_size.restype = ctypes.c_size_t
+    lib.oracle_rand_first.argtypes = [c_int32] * 6 + [c_void_p]
+    lib.oracle_eval_array.argtypes = [c_int32, c_void_p, c_void_p, c_void_p, c_int64]
+    lib.oracle_find_intersection.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int64]
+    lib.oracle_find_intersection.restype = ctypes.c_int
+    lib.oracle_rand_drct.argtypes = [c_void_p, c_void_p]
+    lib.oracle_render.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, POINTER(c_uint64), c_int32,
+                                  POINTER(c_uint64), c_void_p]
+    lib.oracle_render.restype = ctypes.c_int
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = load()
+    return _lib
+
+
+def hash_u32(x: int) -> int:
+    return lib().oracle_hash(x & 0xFFFFFFFF)
+
+
+def rand_first(W, H, seed, x, y, n):
+    out = np.zeros(n, np.float32)
+    lib().oracle_rand_first(W, H, seed, x, y, n, out.ctypes.data)
+    return out
+
+
+def eval_array(fn: int, x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    aux = np.empty(x.shape, np.int32)
+    lib().oracle_eval_array(fn, x.ctypes.data, out.ctypes.data, aux.ctypes.data, x.size)
+    return out, aux
+
+
+def find_intersection(scene_desc, rays):
+    rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+    out = np.empty((rays.shape[0], 8), np.float32)
+    col = np.empty((rays.shape[0], 3), np.float32)
+    st = lib().oracle_find_intersection(ctypes.addressof(scene_desc), rays.ctypes.data, out.ctypes.data, col.ctypes.data,
+                                        rays.shape[0])
+    assert st == 0
+    return out, col
+
+
+def render(scene_desc, uniforms, reg, frame=None, threads=None, count_ops=False, pixel_counts=False):
+    """Renders `reg` into frame (h, w, 4) float32 (zeros if None). Returns (frame, n_inter, ops, counts)."""
+    h, w = reg.h, reg.w
+    if frame is None:
+        frame = np.zeros((h, w, 4), np.float32)
+    assert frame.dtype == np.float32 and frame.flags["C_CONTIGUOUS"] and frame.shape[0] >= h
+    n = c_uint64()
+    ops = c_uint64()
+    counts = np.zeros((h, w), np.uint32) if pixel_counts else None
+    threads = threads or os.cpu_count() or 1
+    st = lib().oracle_render(ctypes.addressof(scene_desc), ctypes.addressof(uniforms), ctypes.addressof(reg),
+                             frame.ctypes.data, frame.shape[1], threads, ctypes.byref(n), 1 if count_ops else 0,
+                             ctypes.byref(ops), counts.ctypes.data if counts is not None else None)
+    assert st == 0
+    return frame, n.value, ops.value, counts

@@ -1,0 +1,181 @@
+"""HIP kernel vs CPU oracle parity on the MI355X (run on the GPU box: pytest -m gpu).
+
+Bar: bit-exact. Both sides implement the same fp32 contract, so every float the
+kernel produces must have the oracle's bit pattern (NaN == NaN), and intersection counts must match.
+All calls go through the C ABI of librt4.so.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SCENES = ["sphere", "room", "tiger", "cylinder4d", "hypercube"]
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    same = a.view(np.uint32) == b.view(np.uint32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return same | both_nan
+
+
+def assert_bits(a, b, what):
+    eq = bits_equal(a, b)
+    if not eq.all():
+        idx = np.argwhere(~eq)[:5]
+        detail = [(tuple(i), float(np.asarray(a)[tuple(i)]), float(np.asarray(b)[tuple(i)])) for i in idx]
+        pytest.fail(f"{what}: {(~eq).sum()} of {eq.size} values differ, e.g. {detail}")
+
+
+# ------------------------------------------------------------------------------------------ math
+def test_device_math_bitwise(tracer, rt4, oracle):
+    rng = np.random.default_rng(1)
+    special = np.array([0.0, -0.0, 0.5, -0.5, 1.0, -1.0, 1.0000001, -1.0000001, np.nan, np.inf, -np.inf,
+                        np.float32(0.49999997), np.float32(0.50000006), 1e-30, -1e-30, 1e-40], np.float32)
+    unit = np.concatenate([np.linspace(-1.0, 1.0, 400001, dtype=np.float32), rng.uniform(-1.2, 1.2, 200000).astype(np.float32), special])
+    angles = np.concatenate([np.linspace(-10.0, 10.0, 400001, dtype=np.float32),
+                             (rng.random(200000, dtype=np.float32) * np.float32(2.0) * np.float32(3.14159265)), special])
+    for fn, x in [(rt4.EVAL_ACOS, unit), (rt4.EVAL_ASIN, unit), (rt4.EVAL_SIN, angles), (rt4.EVAL_COS, angles),
+                  (rt4.EVAL_VOLUME_BY_W, unit)]:
+        g, _ = tracer.debug_eval(fn, x)
+        c, _ = oracle.eval_array(fn, x)
+        assert_bits(g, c, f"eval fn {fn}")
+
+
+def test_hash_bitwise(tracer, rt4, oracle):
+    x = np.random.default_rng(2).integers(0, 2**32, 100000, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    g, _ = tracer.debug_eval(rt4.EVAL_HASH, x)
+    c, _ = oracle.eval_array(rt4.EVAL_HASH, x)
+    assert (g.view(np.uint32) == c.view(np.uint32)).all()
+
+
+def test_w_by_volume_exhaustive(tracer, rt4, oracle):
+    """Every value rand() can return (m * 2^-23, shader.frag:111-118): result bits and Newton iterations."""
+    v = (np.arange(1 << 23, dtype=np.uint32) | np.uint32(0x3F800000)).view(np.float32) - np.float32(1.0)
+    g, gi = tracer.debug_eval(rt4.EVAL_W_BY_VOLUME, v)
+    c, ci = oracle.eval_array(rt4.EVAL_W_BY_VOLUME, v)
+    assert_bits(g, c, "w_by_volume")
+    assert (gi == ci).all()
+    assert not np.isnan(g).any() and np.abs(g).max() <= 1.0
+    assert gi.max() < 64  # the loop cap is never reached
+
+
+# ------------------------------------------------------------------------------- intersections
+def random_rays(n, seed):
+    rng = np.random.default_rng(seed)
+    p = rng.uniform(-4.0, 4.0, (n, 4)).astype(np.float32)
+    p[: n // 4] = np.array([0.0, -2.0, 0.0, 0.0], np.float32)  # camera focus
+    d = rng.normal(size=(n, 4)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    return np.concatenate([p, d], axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_find_intersection_bitwise(rt4, oracle, name):
+    scene = rt4.Scene.builtin(name)
+    t = rt4.Tracer(device=0, scene=scene)
+    try:
+        rays = random_rays(100000, 1000 + SCENES.index(name))
+        g, gc = t.debug_find_intersection(rays)
+        c, cc = oracle.find_intersection(scene.desc, rays)
+        assert_bits(g, c, f"{name} find_intersection")
+        assert_bits(gc, cc, f"{name} material color")
+        assert g[:, 0].sum() > 1000  # the rays do hit things
+    finally:
+        t.close()
+
+
+# -------------------------------------------------------------------------------------- images
+def render_both(rt4, oracle, scene, u, reg, flags=0, old=None):
+    t = rt4.Tracer(device=0, flags=flags, scene=scene)
+    try:
+        fg = np.zeros((reg.h, reg.w, 4), np.float32) if old is None else old.copy()
+        ng = t.render_host(u, reg, fg)
+    finally:
+        t.close()
+    fc = np.zeros((reg.h, reg.w, 4), np.float32) if old is None else old.copy()
+    fc, nc, _, _ = oracle.render(scene.desc, u, reg, fc)
+    return fg, ng, fc, nc
+
+
+@pytest.mark.parametrize("name", SCENES)
+@pytest.mark.parametrize("lut", [False, True])
+def test_render_bitwise_small(rt4, oracle, name, lut):
+    u = rt4.make_uniforms(96, 60, samples=4, reflections=4, seed=777)
+    reg = rt4.region(96, 60)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin(name), u, reg, flags=rt4.FLAG_SAMPLER_LUT if lut else 0)
+    assert ng == nc
+    assert_bits(fg, fc, f"{name} image")
+
+
+def test_render_bitwise_config2_rows(rt4, oracle):
+    """BASELINE config 2 (sphere, 1920x1080, 16 spp, 8 bounces, seed 12345) on every 32nd row."""
+    u = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
+    reg = rt4.region(1920, 34, y0=5, band_rows=1, band_step=32)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin("sphere"), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
+    assert ng == nc
+    assert_bits(fg, fc, "config2 rows")
+
+
+def test_render_bitwise_config3_rows(rt4, oracle):
+    """BASELINE config 3 (hypercube, 1920x1080, 16 spp, 8 bounces) on every 64th row."""
+    u = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
+    reg = rt4.region(1920, 17, y0=11, band_rows=1, band_step=64)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin("hypercube"), u, reg)
+    assert ng == nc
+    assert_bits(fg, fc, "config3 rows")
+
+
+def test_progressive_blend(rt4, oracle):
+    """mix(old_frame, new, part) with part = 1/3 over a non-zero old frame (shader.frag:524-527)."""
+    u = rt4.make_uniforms(64, 40, samples=2, reflections=3, seed=99, part=1.0 / 3.0)
+    reg = rt4.region(64, 40)
+    old = np.random.default_rng(5).random((40, 64, 4), dtype=np.float32)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin("tiger"), u, reg, old=old)
+    assert ng == nc
+    assert_bits(fg, fc, "progressive")
+
+
+def test_banded_regions_tile_the_image(rt4):
+    """Pixel-tile sharding: two interleaved band sets reproduce the full image bit for bit."""
+    u = rt4.make_uniforms(80, 64, samples=2, reflections=3, seed=4242)
+    scene = rt4.Scene.builtin("cylinder4d")
+    t = rt4.Tracer(device=0, scene=scene)
+    try:
+        full = np.zeros((64, 80, 4), np.float32)
+        n_full = t.render_host(u, rt4.region(80, 64), full)
+        parts, n_parts = [], 0
+        for r in range(2):
+            f = np.zeros((32, 80, 4), np.float32)
+            n_parts += t.render_host(u, rt4.region(80, 32, y0=8 * r, band_rows=8, band_step=16), f)
+            parts.append(f)
+    finally:
+        t.close()
+    rebuilt = np.zeros_like(full)
+    for r in range(2):
+        for b in range(4):
+            rebuilt[16 * b + 8 * r: 16 * b + 8 * r + 8] = parts[r][8 * b: 8 * b + 8]
+    assert n_parts == n_full
+    assert_bits(rebuilt, full, "banded")
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_golden_images(rt4, name):
+    """GPU output against the committed oracle images (tests/golden/make_golden.py)."""
+    meta = json.load(open(os.path.join(GOLDEN, "images.json")))[name]
+    u = rt4.make_uniforms(meta["width"], meta["height"], samples=meta["samples"], reflections=meta["reflections"],
+                          seed=meta["seed"])
+    t = rt4.Tracer(device=0, scene=rt4.Scene.builtin(name))
+    try:
+        f = np.zeros((meta["height"], meta["width"], 4), np.float32)
+        n = t.render_host(u, rt4.region(meta["width"], meta["height"]), f)
+    finally:
+        t.close()
+    ref = np.load(os.path.join(GOLDEN, f"image_{name}.npy"))
+    assert n == meta["intersections"]
+    assert_bits(f, ref, f"golden {name}")
