@@ -67,13 +67,17 @@ def cpu_baseline(rt4, scene, u, width, height, target_s):
     step = max(1, height // rows_wanted)
     y0 = 3 % step
     reg = rt4.region(width, len(range(y0, height, step)), y0=y0, band_rows=1, band_step=step)
-    t0 = time.perf_counter()
-    _, n, _, _ = oracle_lib.render(scene.desc, u, reg, threads=threads)
-    dt = time.perf_counter() - t0
+    n, dt, reps = 0, 0.0, 0
+    while dt < target_s and reps < 100:  # a whole frame can take less than the target: repeat it
+        t0 = time.perf_counter()
+        _, k, _, _ = oracle_lib.render(scene.desc, u, reg, threads=threads)
+        dt += time.perf_counter() - t0
+        n += k
+        reps += 1
+    what = "the whole frame" if step == 1 else f"every {step}th row ({reg.h} of {height} rows)"
     return {"value": n / dt, "unit": "ray-bounce intersections/s", "cores": threads, "kind": "port",
-            "sample": f"every {step}th row ({reg.h} of {height} rows) x {width} px of the same frame, {u.samples} spp, "
-                      f"{u.reflections_amount} bounces: {n} intersections in {dt:.1f} s; oracle/rt4_oracle.cpp "
-                      f"(-O3, scalar) on {threads} host threads"}
+            "sample": f"{what} x {width} px, {u.samples} spp, {u.reflections_amount} bounces, rendered {reps}x: "
+                      f"{n} intersections in {dt:.1f} s; oracle/rt4_oracle.cpp (-O3, scalar) on {threads} host threads"}
 
 
 def ops_per_unit(rt4, scene, u, width, height):

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run: per-kernel average duration and PMC-derived metrics.
+
+Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [kernel-substring]
+Writes <dir>/summary.json and prints it. Counter semantics (rocprofv3 -L on gfx950):
+  SQ_INSTS_VALU            VALU wave-instructions issued (all SEs)
+  SQ_THREAD_CYCLES_VALU    VALU thread-cycles (x active lanes)  -> lane utilisation
+  SQ_ACTIVE_INST_VALU      quad-cycles waves spend on VALU
+  SQ_WAVE_CYCLES / SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE            -> occupancy, clock
+  FETCH_SIZE / WRITE_SIZE  KiB from/to the memory side; FETCH_SIZE doubled on gfx950
+                           (MI355X_MICROARCH.md §HBM: it reports 1/2 of wide coalesced reads)
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+CUS, SIMDS_PER_CU, LANES = 256, 4, 64
+
+
+def kernel_rows(path, sub):
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if sub in r.get("Kernel_Name", ""):
+                yield r
+
+
+def main():
+    d = sys.argv[1]
+    sub = sys.argv[2] if len(sys.argv) > 2 else "rt4_trace_kernel"
+    out = {"dir": d, "kernel": sub}
+    tr = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))
+    if tr:
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kernel_rows(tr[0], sub)]
+        if durs:
+            out["dispatches"] = len(durs)
+            out["avg_ns"] = sum(durs) / len(durs)
+            out["min_ns"] = min(durs)
+            out["max_ns"] = max(durs)
+            rows = list(kernel_rows(tr[0], sub))
+            out["vgpr"] = int(rows[0]["VGPR_Count"])
+            out["sgpr"] = int(rows[0]["SGPR_Count"])
+            out["scratch"] = int(rows[0]["Scratch_Size"])
+            out["lds"] = int(rows[0]["LDS_Block_Size"])
+    counters = defaultdict(list)
+    durations = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "pmc_*", "*counter_collection.csv")):
+        for r in kernel_rows(f, sub):
+            counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            durations[r["Counter_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    c = {k: sum(v) / len(v) for k, v in counters.items()}
+    out["counters"] = c
+    m = {}
+    if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
+        m["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+        # ACTIVE_INST_VALU is in quad-cycles; a wave64 VALU op occupies 2 SIMD-32 cycles on 64 lanes
+        m["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 4 * 32)
+    if "GRBM_GUI_ACTIVE" in c:
+        dur = sum(durations["GRBM_GUI_ACTIVE"]) / len(durations["GRBM_GUI_ACTIVE"])
+        m["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / dur  # summed over 8 XCDs (MI355X_MICROARCH.md DVFS note)
+        m["pmc_pass_duration_ns"] = dur
+    if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        dur = sum(durations["SQ_INSTS_VALU"]) / len(durations["SQ_INSTS_VALU"])
+        clk = m.get("clock_ghz", 2.4) * 1e9
+        # each wave64 VALU instruction needs 2 cycles of one SIMD-32
+        m["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 2 / (CUS * SIMDS_PER_CU * clk * dur * 1e-9)
+    if "SQ_WAVE_CYCLES" in c and "SQ_BUSY_CYCLES" in c:
+        m["avg_waves_per_simd"] = c["SQ_WAVE_CYCLES"] * 4 / (c["SQ_BUSY_CYCLES"] * 32 * SIMDS_PER_CU / 32) / 1
+    if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c:
+        m["valu_share_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
+    if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        m["wait_any_share"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+        m["wait_inst_any_share"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+        m["active_any_share"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+    if "FETCH_SIZE" in c:
+        m["hbm_read_bytes_corrected"] = c["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in c:
+        m["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        m["hbm_bytes_per_launch"] = m["hbm_read_bytes_corrected"] + m["hbm_write_bytes"]
+    out["derived"] = m
+    json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,31 @@
+#!/usr/bin/env bash
+# rocprofv3 passes over bench.py (run on the GPU box from the repo root):
+#   1. kernel trace + stats (per-kernel average duration; must agree with bench.py's kernel_ms)
+#   2..n. PMC passes, each its own run with --kernel-trace only (MI355X_MICROARCH.md §rocprofv3 PMC slots)
+# Usage: tools/profile.sh <tag> [bench args...]
+set -u
+TAG=${1:-run}
+shift || true
+ARGS=${*:-"--steps 5 --warmup 1 --no-cpu-baseline"}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+PY=$(command -v python3)
+
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o "$name" --output-format csv -- "$PY" "$ROOT/bench.py" $ARGS \
+    > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  return $rc
+}
+
+run trace --kernel-trace --stats || exit 1
+run pmc_inst --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH || exit 1
+run pmc_cyc --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
+run pmc_thr --kernel-trace --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA || true
+run pmc_fetch --kernel-trace --pmc FETCH_SIZE || exit 1
+run pmc_write --kernel-trace --pmc WRITE_SIZE || exit 1
+echo "profile $TAG done"
