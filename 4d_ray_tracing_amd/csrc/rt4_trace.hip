@@ -2,14 +2,17 @@
 // plus the device context and the C-ABI render / diagnostic entry points of include/rt4.h.
 //
 // Kernel shape:
-//   * one lane per pixel; a 256-thread workgroup renders a 16x16 pixel tile, each wave an 8x8
-//     sub-tile (spatially coherent paths inside a wave).
-//   * the sample x bounce loops of main()/trace() (shader.frag:474, :520) are FLATTENED into one
-//     loop of find_intersection calls: a lane whose path ends starts its next sample in the same
-//     iteration, so a wave runs max_lane(sum of path lengths) iterations, not
-//     samples * max(path length). The RNG counter keeps running across samples (shader.frag:92).
-//   * scene geometry is wave-uniform: read through a const __restrict__ pointer, which the
-//     compiler turns into scalar (s_load / K$) loads; materials are fetched per lane at shading.
+//   * persistent waves over a global pixel queue. One lane traces one pixel at a time. A lane
+//     whose pixel has run all its samples goes idle; once >= REFILL_MIN lanes of a wave are idle,
+//     the wave writes their pixels out and hands them new pixels (ballot + mbcnt rank) from
+//     64-pixel batches (8x8 tiles) claimed with one atomicAdd. Lanes stay busy until the queue
+//     drains, instead of idling until the slowest pixel of a fixed 64-pixel wave is done.
+//   * within a pixel the sample x bounce loops of main()/trace() (shader.frag:474, :520) are
+//     FLATTENED: one loop iteration = one find_intersection + its shading. A finished path starts
+//     the pixel's next sample in the next iteration. The RNG counter keeps running across samples
+//     (shader.frag:92), exactly as in the shader.
+//   * find_intersection is specialised per scene shape (rt4_intersect.h); scene geometry is
+//     wave-uniform -> scalar loads; materials are fetched per lane at shading.
 //   * optional w_by_volume table (RT4_FLAG_SAMPLER_LUT): the Newton loop of shader.frag:141-150
 //     is a pure function of rand()'s 23 mantissa bits; a 2^23-entry table built by the same
 //     device function replaces the divergent loop by one cached load.
@@ -21,184 +24,24 @@
 
 #include "../../include/rt4.h"
 #include "rt4_device_math.h"
+#include "rt4_intersect.h"
 #include "rt4_internal.h"
 
 using namespace rt4;
 
 namespace {
 
-// ---------------------------------------------------------------- hit record
-struct Hit {
-  bool hit;
-  float dist;
-  V4 norm;
-  int mat;  // byte offset of the rt4_material inside the device scene
-};
+constexpr unsigned BATCH = 64;      // pixels per queue claim: one 8x8 tile
+constexpr unsigned REFILL_MIN = 8;  // refill a wave once this many of its lanes are idle
+constexpr uint32_t GENERIC = 0xFFFFFFFFu;
+constexpr int QUEUE_SLOTS = 64;     // rotating per-launch queue words (see rt4_render_device)
 
-__device__ __forceinline__ Hit no_hit() { return Hit{false, 0.0f, V4{0.0f, 0.0f, 0.0f, 0.0f}, 0}; }
-
-// closest(a, b), shader.frag:181-185 (tie -> b)
-__device__ __forceinline__ Hit closest(const Hit& a, const Hit& b) {
-  if (!a.hit) return b;
-  if (!b.hit) return a;
-  return a.dist < b.dist ? a : b;
-}
-
-#define MAT_OFF(ptr) (static_cast<int>(reinterpret_cast<const char*>(&(ptr)) - reinterpret_cast<const char*>(S)))
-
-struct Ray { V4 point, drct; };
-
-// ---------------------------------------------------------------- intersectors (shader.frag:189-400)
-__device__ __forceinline__ Hit sphere_intersection(V4 center, float r, int mat, Ray ray, bool outer) {  // :197-221
-  V4 vec_po = sub(center, ray.point);
-  float len_po = length(vec_po);
-  float cos_opa;
-  if (len_po < SMALL_F) {
-    cos_opa = 0.0f;
-  } else {
-    float dot_pord = dot(vec_po, ray.drct);
-    if (len_po >= r && dot_pord < 0.0f) return no_hit();
-    cos_opa = dot_pord / len_po;
-    cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
-    cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
-  }
-  float angle_opa = acos_(cos_opa);
-  float sin_oap = len_po * sin_(angle_opa) / r;
-  if (sin_oap >= 1.0f) return no_hit();
-  float angle_oap = asin_(sin_oap);
-  bool flip = outer && len_po > r;
-  if (flip) angle_oap = PI_F - angle_oap;
-  float angle_aop = PI_F - angle_opa - angle_oap;
-  float dist = __builtin_sqrtf(r * r + len_po * len_po - 2.0f * r * len_po * cos_(angle_aop));
-  V4 norm = divs(sub(center, mad(ray.drct, dist, ray.point)), r);
-  if (flip) norm = neg(norm);
-  return Hit{true, dist, norm, mat};
-}
-
-__device__ __forceinline__ Hit space_intersection(const rt4_scene_desc* __restrict__ S, int i, Ray ray) {  // :231-239
-  const rt4_space& s = S->spaces[i];
-  V4 sn = ld4(s.norm);
-  float dot_vn = dot(sub(ld4(s.point), ray.point), sn);
-  float sgn = dot_vn > 0.0f ? 1.0f : (dot_vn < 0.0f ? -1.0f : 0.0f);
-  V4 drct_h = mul(sn, sgn);
-  float cos_dh = dot(drct_h, ray.drct);
-  if (cos_dh < SMALL_F) return no_hit();
-  float dist = __builtin_fabsf(dot_vn) / cos_dh;
-  return Hit{true, dist, neg(drct_h), MAT_OFF(s.material)};
-}
-
-__device__ __forceinline__ V4 point_in_space(V4 p, V4 sp, V4 sn) { return mad(sn, dot(sub(sp, p), sn), p); }
-__device__ __forceinline__ V4 vec_in_space(V4 v, V4 sn) { return mad(sn, -dot(v, sn), v); }
-
-__device__ __forceinline__ Hit cylinder_intersection(const rt4_scene_desc* __restrict__ S, const rt4_cylinder& c,
-                                                     Ray ray, bool outer) {  // :251-267
-  V4 cp = ld4(c.point), a1 = ld4(c.axis1), a2 = ld4(c.axis2);
-  Ray r1{point_in_space(ray.point, cp, a1), vec_in_space(ray.drct, a1)};
-  if (length(r1.drct) < SMALL_F) return no_hit();
-  Ray r12{point_in_space(r1.point, cp, a2), vec_in_space(r1.drct, a2)};
-  float len = length(r12.drct);
-  if (len < SMALL_F) return no_hit();
-  r12.drct = divs(r12.drct, len);
-  Hit h = sphere_intersection(cp, c.r, MAT_OFF(c.material), r12, outer);
-  h.dist = h.dist / len;
-  return h;
-}
-
-__device__ __forceinline__ float dist_to_axes_plane(float dist, Ray ray, const rt4_cylinder& c) {  // :270-275
-  V4 cp = ld4(c.point);
-  V4 p = mad(ray.drct, dist, ray.point);
-  V4 p1 = point_in_space(p, cp, ld4(c.axis1));
-  V4 p12 = point_in_space(p1, cp, ld4(c.axis2));
-  return length(sub(cp, p12));
-}
-
-__device__ __forceinline__ Hit cylinders_union_intersection(const rt4_scene_desc* __restrict__ S, int i,
-                                                            Ray ray) {  // :284-294
-  const rt4_cylinders_union& u = S->unions[i];
-  Hit i1 = cylinder_intersection(S, u.cylinder1, ray, true);
-  if (dist_to_axes_plane(i1.dist, ray, u.cylinder2) > u.cylinder2.r) i1 = no_hit();
-  Hit i2 = cylinder_intersection(S, u.cylinder2, ray, true);
-  if (dist_to_axes_plane(i2.dist, ray, u.cylinder1) > u.cylinder2.r) i2 = no_hit();  // :290 (cylinder2.r)
-  return closest(i1, i2);
-}
-
-__device__ __forceinline__ Hit tigers_face(const rt4_scene_desc* __restrict__ S, const rt4_cylinder& cyl,
-                                           const rt4_cylinder& outer_cyl, const rt4_cylinder& inner_cyl, Ray ray,
-                                           bool outer) {  // :317-324
-  Hit h = cylinder_intersection(S, cyl, ray, outer);
-  if (dist_to_axes_plane(h.dist, ray, outer_cyl) > outer_cyl.r) return no_hit();
-  if (dist_to_axes_plane(h.dist, ray, inner_cyl) < inner_cyl.r) return no_hit();
-  return h;
-}
-
-__device__ __forceinline__ Hit tiger_intersection(const rt4_scene_desc* __restrict__ S, int i, Ray ray) {  // :327-341
-  const rt4_tiger& t = S->tigers[i];
-  Hit i111 = tigers_face(S, t.inner_cyl1, t.outer_cyl2, t.inner_cyl2, ray, true);
-  Hit i112 = tigers_face(S, t.inner_cyl1, t.outer_cyl2, t.inner_cyl2, ray, false);
-  Hit i121 = tigers_face(S, t.outer_cyl1, t.outer_cyl2, t.inner_cyl2, ray, true);
-  Hit i122 = tigers_face(S, t.outer_cyl1, t.outer_cyl2, t.inner_cyl2, ray, false);
-  Hit i211 = tigers_face(S, t.inner_cyl2, t.outer_cyl1, t.inner_cyl1, ray, true);
-  Hit i212 = tigers_face(S, t.inner_cyl2, t.outer_cyl1, t.inner_cyl1, ray, false);
-  Hit i221 = tigers_face(S, t.outer_cyl2, t.outer_cyl1, t.inner_cyl1, ray, true);
-  Hit i222 = tigers_face(S, t.outer_cyl2, t.outer_cyl1, t.inner_cyl1, ray, false);
-  return closest(closest(closest(i111, i112), closest(i121, i122)), closest(closest(i211, i212), closest(i221, i222)));
-}
-
-__device__ __forceinline__ Hit cube_intersection(const rt4_scene_desc* __restrict__ S, const rt4_cube& c,
-                                                 Ray ray) {  // :352-366
-  V4 cpt = ld4(c.point), cn = ld4(c.norm);
-  V4 vec_n = neg(cn);
-  float h = dot(sub(cpt, ray.point), vec_n);
-  if (h < 0.0f) return no_hit();
-  float cos_dn = dot(ray.drct, vec_n);
-  if (cos_dn < 0.0f) return no_hit();
-  float dist = h / cos_dn;
-  V4 vec_cp = sub(mad(ray.drct, dist, ray.point), cpt);
-  if (__builtin_fabsf(dot(vec_cp, ld4(c.x))) > c.r) return no_hit();
-  if (__builtin_fabsf(dot(vec_cp, ld4(c.y))) > c.r) return no_hit();
-  if (__builtin_fabsf(dot(vec_cp, ld4(c.z))) > c.r) return no_hit();
-  return Hit{true, dist, cn, MAT_OFF(c.material)};
-}
-
-__device__ __forceinline__ Hit hypercube_intersection(const rt4_scene_desc* __restrict__ S, int i, Ray ray) {  // :394-400
-  const rt4_hypercube& hc = S->hypercubes[i];
-  Hit res = no_hit();
-  for (int k = 0; k < 8; k++) {
-    Hit h = cube_intersection(S, hc.cubes[k], ray);
-    if (!res.hit && h.hit) res = h;  // first hit in cell order
-  }
-  return res;
-}
-
-__device__ __forceinline__ Hit find_intersection(const rt4_scene_desc* __restrict__ S, Ray ray) {  // :434-451
-  Hit inter = no_hit();
-  const int ng = S->n_groups;
-  for (int g = 0; g < ng; g++) {
-    const int kind = S->groups[g].kind, first = S->groups[g].first, count = S->groups[g].count;
-    const bool outer = S->groups[g].outer != 0, new_first = S->groups[g].new_first != 0;
-    for (int k = 0; k < count; k++) {
-      const int i = first + k;
-      Hit n;
-      if (kind == RT4_GROUP_SPACES) {
-        n = space_intersection(S, i, ray);
-      } else if (kind == RT4_GROUP_SPHERES) {
-        const rt4_sphere& sp = S->spheres[i];
-        n = sphere_intersection(ld4(sp.center), sp.r, MAT_OFF(sp.material), ray, outer);
-      } else if (kind == RT4_GROUP_CYLINDERS) {
-        n = cylinder_intersection(S, S->cylinders[i], ray, outer);
-      } else if (kind == RT4_GROUP_CYLINDERS_UNION) {
-        n = cylinders_union_intersection(S, i, ray);
-      } else if (kind == RT4_GROUP_HYPERCUBE) {
-        n = hypercube_intersection(S, i, ray);
-      } else if (kind == RT4_GROUP_TIGER) {
-        n = tiger_intersection(S, i, ray);
-      } else {
-        continue;
-      }
-      inter = new_first ? closest(n, inter) : closest(inter, n);
-    }
-  }
-  return inter;
+template <uint32_t K>
+__device__ __forceinline__ Hit find_intersection(const rt4_scene_desc* __restrict__ S, const Ray& ray) {
+  if constexpr (K == GENERIC)
+    return find_intersection_generic(S, ray);
+  else
+    return find_intersection_spec<K>(S, ray);
 }
 
 // ---------------------------------------------------------------- shading (shader.frag:404-495)
@@ -223,25 +66,21 @@ struct RngState {
   uint32_t iter;  // rand_iter_seed                                (shader.frag:92, :105)
 };
 
-__device__ __forceinline__ float rand_(RngState& r) {  // :104-118
+__device__ __forceinline__ uint32_t rand_bits(RngState& r) {  // 23 mantissa bits of rand(), :104-116
   r.iter += 0x79A010A9u;
-  uint32_t bits = hash_u32(r.base ^ r.iter);
-  return __uint_as_float((bits & 0x007FFFFFu) | 0x3F800000u) - 1.0f;
+  return hash_u32(r.base ^ r.iter) & 0x007FFFFFu;
 }
+__device__ __forceinline__ float bits_to_rand(uint32_t m) { return __uint_as_float(m | 0x3F800000u) - 1.0f; }  // :117
+__device__ __forceinline__ float rand_(RngState& r) { return bits_to_rand(rand_bits(r)); }
 
 template <bool LUT>
 __device__ __forceinline__ V4 rand_drct(RngState& rng, const float* __restrict__ wlut) {  // :153-158
-  float u1 = rand_(rng);
-  float w;
-  if (LUT) {
-    w = wlut[__float_as_uint(u1 + 1.0f) & 0x007FFFFFu];  // u1 = m * 2^-23 exactly
-  } else {
-    w = w_by_volume(u1, nullptr);
-  }
-  float r = __builtin_sqrtf(1.0f - w * w);
-  float z = (rand_(rng) * 2.0f - 1.0f) * r;
-  float rr = __builtin_sqrtf(r * r - z * z);
-  float fi = rand_(rng) * 2.0f * PI_F;
+  const uint32_t m = rand_bits(rng);
+  const float w = LUT ? wlut[m] : w_by_volume(bits_to_rand(m), nullptr);
+  const float r = __builtin_sqrtf(1.0f - w * w);
+  const float z = (rand_(rng) * 2.0f - 1.0f) * r;
+  const float rr = __builtin_sqrtf(r * r - z * z);
+  const float fi = rand_(rng) * 2.0f * PI_F;
   float sf, cf;
   sincos_(fi, sf, cf);
   return V4{rr * cf, rr * sf, z, w};
@@ -253,93 +92,154 @@ struct KernelArgs {
   int64_t row_stride_px;
 };
 
-template <bool LUT>
+__device__ __forceinline__ int region_row(const rt4_region& r, int i) {
+  return r.band_rows > 0 ? r.y0 + (i / r.band_rows) * r.band_step + (i % r.band_rows) : r.y0 + i;
+}
+
+// light /= samples; light_to_color; mix(old_frame, new, part); alpha 1 (shader.frag:522-527)
+__device__ __forceinline__ void write_pixel(const KernelArgs& a, float4* __restrict__ frame, int j, int i, V3 light) {
+  const float ns = static_cast<float>(a.u.samples);
+  light = V3{light.x / ns, light.y / ns, light.z / ns};
+  const float k = a.u.light_to_color_conversion_coefficient;
+  const V3 c{1.0f - 1.0f / fmaf_(k, light.x, 1.0f), 1.0f - 1.0f / fmaf_(k, light.y, 1.0f),
+             1.0f - 1.0f / fmaf_(k, light.z, 1.0f)};
+  float4* px = frame + static_cast<int64_t>(i) * a.row_stride_px + j;
+  const float4 old = *px;
+  const float part = a.u.part, keep = 1.0f - a.u.part;
+  *px = make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep), fmaf_(c.z, part, old.z * keep),
+                    1.0f);
+}
+
+template <uint32_t K, bool LUT>
 __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S, const KernelArgs a,
                                                         float4* __restrict__ frame,
                                                         unsigned long long* __restrict__ counter,
-                                                        const float* __restrict__ wlut) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  const int i = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-  const bool active = (j < a.reg.w) && (i < a.reg.h);
-
-  const int x = a.reg.x0 + j;
-  const int y = a.reg.band_rows > 0 ? a.reg.y0 + (i / a.reg.band_rows) * a.reg.band_step + (i % a.reg.band_rows)
-                                    : a.reg.y0 + i;
-  // main(): scr_coord = gl_FragCoord.xy / resolution (shader.frag:515-516)
-  const float sx = (static_cast<float>(x) + 0.5f) / a.u.resolution[0];
-  const float sy = (static_cast<float>(y) + 0.5f) / a.u.resolution[1];
-  const uint32_t useed = static_cast<uint32_t>(a.u.seed);
-  RngState rng{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ useed, useed};
-
-  // ray_drct(), shader.frag:501-505
-  const float mx = (sx - 0.5f) * a.u.mtr_sizes[0];
-  const float my = (0.5f - sy) * a.u.mtr_sizes[1];
-  V4 d0 = mad(ld4(a.u.right_drct), mx, mad(ld4(a.u.top_drct), my, ld4(a.u.vec_to_mtr)));
-  d0 = divs(d0, length(d0));
+                                                        const float* __restrict__ wlut, unsigned* __restrict__ queue) {
+  const unsigned lane = threadIdx.x & 63u;
+  const int W = a.reg.w, H = a.reg.h;
+  const unsigned tiles_x = (static_cast<unsigned>(W) + 7u) >> 3;
+  const unsigned total = tiles_x * ((static_cast<unsigned>(H) + 7u) >> 3) * 64u;
   const V4 focus = ld4(a.u.focus);
-
-  // flattened samples x bounces (shader.frag:520-521 around :474-495)
-  Ray ray{focus, d0};
-  V3 acc{0.0f, 0.0f, 0.0f}, T{1.0f, 1.0f, 1.0f}, light{0.0f, 0.0f, 0.0f};
-  int s = active ? 0 : a.u.samples;
-  int b = 0;
-  uint32_t n_inter = 0;
   const float indent = a.u.small_indent;
-  const int R = a.u.reflections_amount;
+  const int R = a.u.reflections_amount, NS = a.u.samples;
+  const uint32_t useed = static_cast<uint32_t>(a.u.seed);
   const char* Sb = reinterpret_cast<const char*>(S);
 
-  while (s < a.u.samples) {
-    Hit h = find_intersection(S, ray);
-    ++n_inter;
-    bool end;
-    if (!h.hit) {  // :477-479
-      V3 fl = final_light(S, ray.drct);
-      acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
-      end = true;
-    } else {
-      const rt4_material* m = reinterpret_cast<const rt4_material*>(Sb + h.mat);
-      const float glow = m->glow, refl = m->refl_prob;
-      const V3 c{m->color[0], m->color[1], m->color[2]};
-      acc = V3{fmaf_(c.x * glow, T.x, acc.x), fmaf_(c.y * glow, T.y, acc.y), fmaf_(c.z * glow, T.z, acc.z)};  // :481
-      T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
-      ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                  // :485
-      if (!(rand_(rng) > refl)) {  // :488 rand_outcome
-        float dn = dot(h.norm, ray.drct);
-        ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);  // reflect
-      } else {
-        V4 v = rand_drct<LUT>(rng, wlut);  // :491 redirect(rand_drct(), norm)
-        float dv = dot(v, h.norm);
-        ray.drct = dv >= 0.0f ? v : mad(h.norm, -(2.0f * dv), v);
+  unsigned b_next = 0, b_end = 0;  // wave-uniform: unclaimed part of the current batch
+  bool exhausted = false;
+  bool active = false, pending = false;
+  int pj = 0, pi = 0;
+  RngState rng{0u, 0u};
+  V4 d0{0.0f, 0.0f, 0.0f, 0.0f};
+  Ray ray{d0, d0};
+  V3 acc{0.0f, 0.0f, 0.0f}, T{1.0f, 1.0f, 1.0f}, light{0.0f, 0.0f, 0.0f};
+  int s = 0, b = 0;
+  uint32_t n_inter = 0;
+
+  while (true) {
+    if (!exhausted) {
+      const unsigned long long idle = __ballot(!active);
+      if (static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN) {
+        if (pending) {
+          write_pixel(a, frame, pj, pi, light);
+          pending = false;
+        }
+        const unsigned rank =
+            __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(idle >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(idle), 0u));
+        const unsigned nidle = static_cast<unsigned>(__popcll(idle));
+        unsigned got = 0;
+        while (got < nidle) {
+          if (b_next == b_end) {
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(queue, BATCH);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base >= total) {
+              exhausted = true;
+              break;
+            }
+            b_next = base;
+            b_end = min(base + BATCH, total);
+          }
+          const unsigned n = min(nidle - got, b_end - b_next);
+          if (!active && rank >= got && rank < got + n) {
+            const unsigned idx = b_next + (rank - got);
+            const unsigned tile = idx >> 6, l = idx & 63u;
+            const int jj = static_cast<int>((tile % tiles_x) * 8u + (l & 7u));
+            const int ii = static_cast<int>((tile / tiles_x) * 8u + (l >> 3));
+            if (jj < W && ii < H) {
+              pj = jj;
+              pi = ii;
+              // main(): scr_coord = gl_FragCoord.xy / resolution (shader.frag:515-516)
+              const float sx = (static_cast<float>(a.reg.x0 + jj) + 0.5f) / a.u.resolution[0];
+              const float sy = (static_cast<float>(region_row(a.reg, ii)) + 0.5f) / a.u.resolution[1];
+              rng = RngState{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ useed, useed};
+              // ray_drct(), shader.frag:501-505
+              const float mx = (sx - 0.5f) * a.u.mtr_sizes[0];
+              const float my = (0.5f - sy) * a.u.mtr_sizes[1];
+              d0 = mad(ld4(a.u.right_drct), mx, mad(ld4(a.u.top_drct), my, ld4(a.u.vec_to_mtr)));
+              d0 = divs(d0, length(d0));
+              ray = Ray{focus, d0};
+              acc = V3{0.0f, 0.0f, 0.0f};
+              T = V3{1.0f, 1.0f, 1.0f};
+              light = V3{0.0f, 0.0f, 0.0f};
+              s = 0;
+              b = 0;
+              active = NS > 0;
+              pending = !active;
+            }
+          }
+          b_next += n;
+          got += n;
+        }
       }
-      ++b;
-      end = b > R;
     }
-    if (end) {  // path finished: next sample restarts at the focus
-      light = V3{light.x + acc.x, light.y + acc.y, light.z + acc.z};
-      ++s;
-      b = 0;
-      ray = Ray{focus, d0};
-      acc = V3{0.0f, 0.0f, 0.0f};
-      T = V3{1.0f, 1.0f, 1.0f};
+    if (!__any(active)) {
+      if (exhausted) break;
+      continue;
+    }
+    if (active) {
+      Hit h = find_intersection<K>(S, ray);  // :475
+      ++n_inter;
+      bool end;
+      if (!h.hit) {  // :477-479
+        const V3 fl = final_light(S, ray.drct);
+        acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
+        end = true;
+      } else {
+        const rt4_material* m = reinterpret_cast<const rt4_material*>(Sb + h.mat);
+        const float glow = m->glow, refl = m->refl_prob;
+        const V3 c{m->color[0], m->color[1], m->color[2]};
+        acc = V3{fmaf_(c.x * glow, T.x, acc.x), fmaf_(c.y * glow, T.y, acc.y), fmaf_(c.z * glow, T.z, acc.z)};  // :481
+        T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
+        ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                  // :485
+        if (!(rand_(rng) > refl)) {  // :488 rand_outcome -> reflect
+          const float dn = dot(h.norm, ray.drct);
+          ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
+        } else {  // :491 redirect(rand_drct(), norm)
+          const V4 v = rand_drct<LUT>(rng, wlut);
+          const float dv = dot(v, h.norm);
+          ray.drct = dv >= 0.0f ? v : mad(h.norm, -(2.0f * dv), v);
+        }
+        ++b;
+        end = b > R;
+      }
+      if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
+        light = V3{light.x + acc.x, light.y + acc.y, light.z + acc.z};
+        ++s;
+        b = 0;
+        ray = Ray{focus, d0};
+        acc = V3{0.0f, 0.0f, 0.0f};
+        T = V3{1.0f, 1.0f, 1.0f};
+        if (s >= NS) {
+          active = false;
+          pending = true;
+        }
+      }
     }
   }
+  if (pending) write_pixel(a, frame, pj, pi, light);
 
-  if (active) {
-    const float ns = static_cast<float>(a.u.samples);
-    light = V3{light.x / ns, light.y / ns, light.z / ns};  // :522
-    const float k = a.u.light_to_color_conversion_coefficient;  // :509-511
-    const V3 c{1.0f - 1.0f / fmaf_(k, light.x, 1.0f), 1.0f - 1.0f / fmaf_(k, light.y, 1.0f),
-               1.0f - 1.0f / fmaf_(k, light.z, 1.0f)};
-    float4* px = frame + static_cast<int64_t>(i) * a.row_stride_px + j;
-    const float4 old = *px;  // old_frame (:526)
-    const float part = a.u.part, keep = 1.0f - a.u.part;
-    *px = make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep),
-                      fmaf_(c.z, part, old.z * keep), 1.0f);  // mix, alpha 1 (:527)
-  }
-
-  if (counter) {
-    // wave-level sum, one atomic per wave
+  if (counter) {  // wave-level sum, one atomic per wave
     unsigned long long v = n_inter;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(counter, v);
@@ -372,12 +272,13 @@ __global__ void rt4_eval_kernel(int fn, const float* __restrict__ in, float* __r
   if (aux) aux[t] = it;
 }
 
+template <uint32_t K>
 __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const float* __restrict__ rays,
                                 float* __restrict__ out, float* __restrict__ out_color, int64_t n) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const float* r = rays + 8 * t;
-  Hit h = find_intersection(S, Ray{ld4(r), ld4(r + 4)});
+  Hit h = find_intersection<K>(S, Ray{ld4(r), ld4(r + 4)});
   float* o = out + 8 * t;
   o[0] = h.hit ? 1.0f : 0.0f;
   o[1] = h.dist;
@@ -392,6 +293,71 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const floa
   }
 }
 
+// ---------------------------------------------------------------- kernel table
+typedef void (*TraceFn)(const rt4_scene_desc*, const KernelArgs, float4*, unsigned long long*, const float*, unsigned*);
+typedef void (*FindFn)(const rt4_scene_desc*, const float*, float*, float*, int64_t);
+
+struct Variant {
+  uint32_t shape;
+  TraceFn trace[2];  // [lut]
+  FindFn find;
+};
+
+#define RT4_VARIANT(K) {K, {rt4_trace_kernel<K, false>, rt4_trace_kernel<K, true>}, rt4_find_kernel<K>}
+const Variant kVariants[] = {
+    RT4_VARIANT(GENERIC),
+    RT4_VARIANT(K_SPACES),
+    RT4_VARIANT(K_SPACES | K_SPHERES),
+    RT4_VARIANT(K_SPACES | K_UNION),
+    RT4_VARIANT(K_SPACES | K_HYPERCUBE),
+    RT4_VARIANT(K_SPACES | K_TIGER),
+    RT4_VARIANT(K_SPACES | K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE | K_TIGER),
+};
+#undef RT4_VARIANT
+
+bool same4(const float* a, const float* b) { return std::memcmp(a, b, 4 * sizeof(float)) == 0; }
+
+// Shape of a scene for the specialised kernels (rt4_intersect.h: find_intersection_spec); GENERIC
+// when the group list is anything other than shader.frag's canonical form.
+uint32_t scene_shape(const rt4_scene_desc& s) {
+  static const uint32_t bit[7] = {0, K_SPACES, K_SPHERES, K_CYLINDERS, K_UNION, K_HYPERCUBE, K_TIGER};
+  uint32_t k = 0;
+  int last = 0;
+  for (int g = 0; g < s.n_groups; g++) {
+    const rt4_group& gr = s.groups[g];
+    if (gr.kind <= last || gr.kind > RT4_GROUP_TIGER || !gr.new_first || gr.first != 0) return GENERIC;
+    last = gr.kind;
+    int n = 0;
+    switch (gr.kind) {
+      case RT4_GROUP_SPACES: n = s.n_spaces; break;
+      case RT4_GROUP_SPHERES: n = s.n_spheres; if (!gr.outer) return GENERIC; break;
+      case RT4_GROUP_CYLINDERS: n = s.n_cylinders; if (!gr.outer) return GENERIC; break;
+      case RT4_GROUP_CYLINDERS_UNION: n = s.n_unions; if (n != 1) return GENERIC; break;
+      case RT4_GROUP_HYPERCUBE: n = s.n_hypercubes; if (n != 1) return GENERIC; break;
+      case RT4_GROUP_TIGER: {
+        n = s.n_tigers;
+        if (n != 1) return GENERIC;
+        const rt4_tiger& t = s.tigers[0];
+        if (!same4(t.inner_cyl1.point, t.outer_cyl1.point) || !same4(t.inner_cyl1.axis1, t.outer_cyl1.axis1) ||
+            !same4(t.inner_cyl1.axis2, t.outer_cyl1.axis2) || !same4(t.inner_cyl2.point, t.outer_cyl2.point) ||
+            !same4(t.inner_cyl2.axis1, t.outer_cyl2.axis1) || !same4(t.inner_cyl2.axis2, t.outer_cyl2.axis2))
+          return GENERIC;
+      } break;
+    }
+    if (gr.count != n) return GENERIC;
+    k |= bit[gr.kind];
+  }
+  for (const Variant& v : kVariants)
+    if (v.shape == k) return k;
+  return GENERIC;
+}
+
+const Variant& variant_for(uint32_t shape) {
+  for (const Variant& v : kVariants)
+    if (v.shape == shape) return v;
+  return kVariants[0];
+}
+
 }  // namespace
 
 // ==================================================================================== context
@@ -400,7 +366,11 @@ struct rt4_context {
   uint32_t flags = 0;
   rt4_scene_desc* d_scene = nullptr;
   bool has_scene = false;
+  uint32_t shape = GENERIC;
   float* d_wlut = nullptr;
+  unsigned* d_queue = nullptr;  // QUEUE_SLOTS words
+  unsigned launch_seq = 0;
+  int n_cu = 0;
 };
 
 #define HIP_TRY(expr)                                                                            \
@@ -428,7 +398,9 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (!c) return rt4_set_err(err, errlen, "out of host memory"), RT4_ERR_ARG;
   c->device = device;
   c->flags = flags;
-  hipError_t e = hipMalloc(&c->d_scene, sizeof(rt4_scene_desc));
+  hipError_t e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
+  if (e == hipSuccess) e = hipMalloc(&c->d_scene, sizeof(rt4_scene_desc));
+  if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess && (flags & RT4_FLAG_SAMPLER_LUT)) {
     e = hipMalloc(&c->d_wlut, sizeof(float) << 23);
     if (e == hipSuccess) {
@@ -451,6 +423,7 @@ void rt4_context_destroy(rt4_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->d_scene) (void)hipFree(ctx->d_scene);
   if (ctx->d_wlut) (void)hipFree(ctx->d_wlut);
+  if (ctx->d_queue) (void)hipFree(ctx->d_queue);
   delete ctx;
 }
 
@@ -460,6 +433,7 @@ int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* e
   if (st != RT4_OK) return st;
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipMemcpy(ctx->d_scene, scene, sizeof(rt4_scene_desc), hipMemcpyHostToDevice));
+  ctx->shape = (ctx->flags & RT4_FLAG_GENERIC_KERNEL) ? GENERIC : scene_shape(*scene);
   ctx->has_scene = true;
   return RT4_OK;
 }
@@ -475,14 +449,20 @@ int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region*
   a.u = *u;
   a.reg = *region;
   a.row_stride_px = row_stride_px;
-  dim3 grid((region->w + 15) / 16, (region->h + 15) / 16);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (ctx->d_wlut)
-    hipLaunchKernelGGL(rt4_trace_kernel<true>, grid, dim3(256), 0, s, ctx->d_scene, a,
-                       reinterpret_cast<float4*>(d_rgba), d_counter, ctx->d_wlut);
-  else
-    hipLaunchKernelGGL(rt4_trace_kernel<false>, grid, dim3(256), 0, s, ctx->d_scene, a,
-                       reinterpret_cast<float4*>(d_rgba), d_counter, ctx->d_wlut);
+  const Variant& v = variant_for(ctx->shape);
+  const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0];
+  // grid: what the device holds at once; later blocks would only find the queue empty
+  int per_cu = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), 256, 0));
+  const long long tiles = static_cast<long long>((region->w + 7) / 8) * ((region->h + 7) / 8);
+  long long blocks = static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1);
+  if (blocks > (tiles + 3) / 4) blocks = (tiles + 3) / 4;  // >= one tile per wave
+  if (blocks < 1) blocks = 1;
+  unsigned* q = ctx->d_queue + (ctx->launch_seq++ % QUEUE_SLOTS);
+  HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, a,
+                     reinterpret_cast<float4*>(d_rgba), d_counter, ctx->d_wlut, q);
   HIP_TRY(hipGetLastError());
   return RT4_OK;
 }
@@ -567,7 +547,7 @@ int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out,
   if (e == hipSuccess) e = hipMalloc(&dcol, n * 3 * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(dr, rays, n * 8 * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(rt4_find_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, 0, ctx->d_scene,
+    hipLaunchKernelGGL(variant_for(ctx->shape).find, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, 0, ctx->d_scene,
                        dr, dout, dcol, n);
     e = hipGetLastError();
   }

@@ -73,6 +73,7 @@ GROUP_SPACES, GROUP_SPHERES, GROUP_CYLINDERS, GROUP_CYLINDERS_UNION, GROUP_HYPER
 FINAL_LIGHT_SUN_SKY, FINAL_LIGHT_CONSTANT = 0, 1
 SECTION_YXZ, SECTION_YWZ, SECTION_YXW = 0, 1, 2
 FLAG_SAMPLER_LUT = 0x1
+FLAG_GENERIC_KERNEL = 0x2
 EVAL_ACOS, EVAL_ASIN, EVAL_SIN, EVAL_COS, EVAL_VOLUME_BY_W, EVAL_W_BY_VOLUME, EVAL_HASH = range(7)
 
 

@@ -240,6 +240,9 @@ typedef struct rt4_context rt4_context;
  * 2^23 values (shader.frag:111-118), so a 32 MiB table built on the device at context creation
  * by the same device function reproduces every Newton result bit for bit. */
 #define RT4_FLAG_SAMPLER_LUT 0x1u
+/* Always use the generic find_intersection (any group list) instead of the kernel specialised for
+ * the scene's shape. Results are identical; used by the tests to cover both code paths. */
+#define RT4_FLAG_GENERIC_KERNEL 0x2u
 
 int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err, size_t errlen);
 int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* err, size_t errlen);

@@ -76,9 +76,10 @@ def random_rays(n, seed):
 
 
 @pytest.mark.parametrize("name", SCENES)
-def test_find_intersection_bitwise(rt4, oracle, name):
+@pytest.mark.parametrize("generic", [False, True])
+def test_find_intersection_bitwise(rt4, oracle, name, generic):
     scene = rt4.Scene.builtin(name)
-    t = rt4.Tracer(device=0, scene=scene)
+    t = rt4.Tracer(device=0, scene=scene, flags=rt4.FLAG_GENERIC_KERNEL if generic else 0)
     try:
         rays = random_rays(100000, 1000 + SCENES.index(name))
         g, gc = t.debug_find_intersection(rays)
@@ -104,11 +105,12 @@ def render_both(rt4, oracle, scene, u, reg, flags=0, old=None):
 
 
 @pytest.mark.parametrize("name", SCENES)
-@pytest.mark.parametrize("lut", [False, True])
-def test_render_bitwise_small(rt4, oracle, name, lut):
+@pytest.mark.parametrize("flags", ["lut", "inline", "generic"])
+def test_render_bitwise_small(rt4, oracle, name, flags):
     u = rt4.make_uniforms(96, 60, samples=4, reflections=4, seed=777)
     reg = rt4.region(96, 60)
-    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin(name), u, reg, flags=rt4.FLAG_SAMPLER_LUT if lut else 0)
+    f = {"lut": rt4.FLAG_SAMPLER_LUT, "inline": 0, "generic": rt4.FLAG_GENERIC_KERNEL}[flags]
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin(name), u, reg, flags=f)
     assert ng == nc
     assert_bits(fg, fc, f"{name} image")
 
