@@ -1,0 +1,36 @@
+// rt4_aux.h — per-scene constants derived on the host at rt4_context_set_scene, stored on the device
+// right after the rt4_scene_desc. They let the specialised kernel replace expensive correctly
+// rounded operations by cheaper ones WITHOUT changing a single result bit:
+//   DivC       x / b for a scene constant b (a radius, the sun's angular size) as
+//              q = x*y, r = fma(-q, b, x), q + r*y with y = RN(1/b). Enabled per divisor only after
+//              an exhaustive device check over all 2^32 numerators found no bit difference against
+//              the IEEE quotient (rt4_verify_div_kernel); otherwise the kernel divides normally.
+//   thresholds sqrt(x) > r  <=>  x > gt(r)   and   sqrt(x) < r  <=>  x < lt(r), exact because
+//              RN(sqrt(.)) is monotone; gt/lt found by bisection over float bit patterns.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/rt4.h"
+
+namespace rt4 {
+
+struct DivC {
+  float b;       // divisor
+  float y;       // RN(1/b)
+  int32_t fast;  // 1: the 3-op quotient was verified bit-exact for every float numerator
+  int32_t pad;
+};
+
+struct SceneAux {
+  DivC sphere_r[RT4_MAX_SPHERES];
+  DivC cyl_r[RT4_MAX_CYLINDERS];
+  DivC union_r[RT4_MAX_UNIONS][2];
+  float union_gt[RT4_MAX_UNIONS];      // gt(cylinder2.r): both union checks use cylinder2.r (shader.frag:286,290)
+  DivC tiger_r[RT4_MAX_TIGERS][4];     // inner_cyl1, outer_cyl1, inner_cyl2, outer_cyl2
+  float tiger_gt[RT4_MAX_TIGERS][2];   // [0]: gt(outer_cyl2.r) filters faces 1xx; [1]: gt(outer_cyl1.r) filters 2xx
+  float tiger_lt[RT4_MAX_TIGERS][2];   // [0]: lt(inner_cyl2.r);                    [1]: lt(inner_cyl1.r)
+  DivC sun_ang;
+};
+
+}  // namespace rt4

@@ -1,0 +1,331 @@
+// rt4_fast.h — the specialised find_intersection (shader.frag:434-451) for scenes in canonical form.
+//
+// Same results as rt4_intersect.h bit for bit; less work, by structure only:
+//   * candidates carry {hit, flip, dist, sdist, id}; the normal and the material are computed once,
+//     for the winning candidate (resolve()), instead of for every primitive hit along the way;
+//   * divisions by scene constants use DivC (rt4_aux.h), verified exhaustively per divisor;
+//   * dist_to_axes_plane(..) > r / < r compare the squared length with exact thresholds (no sqrt);
+//   * tiger: projection / sphere-core / axes-distance shared inside each axes pair (init_tiger).
+#pragma once
+
+#include "rt4_aux.h"
+#include "rt4_intersect.h"
+
+namespace rt4 {
+
+// x / b with the verified 3-op form when allowed (uniform branch: c.fast is a scene constant).
+__device__ __forceinline__ float div_c(float x, const DivC& c) {
+  if (c.fast) {
+    const float q = x * c.y;
+    const float r = fmaf_(-q, c.b, x);
+    const float q2 = fmaf_(r, c.y, q);
+    return (r == 0.0f || !__builtin_isfinite(q)) ? q : q2;
+  }
+  return x / c.b;
+}
+__device__ __forceinline__ V4 divs_c(V4 a, const DivC& c) {
+  return V4{div_c(a.x, c), div_c(a.y, c), div_c(a.z, c), div_c(a.w, c)};
+}
+
+enum : uint32_t {
+  ID_SPACE = 0u,
+  ID_SPHERE = 1u,
+  ID_CYL = 2u,
+  ID_UNION = 3u,   // idx = union*2 + which cylinder
+  ID_CUBE = 4u,    // idx = hypercube*8 + cell
+  ID_TIGER = 5u,   // idx = tiger*4 + (pair*2 + outer_radius)
+};
+__device__ __forceinline__ uint32_t make_id(uint32_t kind, uint32_t idx) { return (kind << 24) | idx; }
+
+struct Cand {
+  bool hit;
+  bool flip;    // sphere-like: normal negated (outer && len_po > r); space: sign(dot_vn) < 0
+  float dist;   // distance along the ray (what closest() compares)
+  float sdist;  // cylinder-like: distance inside the projected 2-plane (before /= len)
+  uint32_t id;
+};
+
+__device__ __forceinline__ Cand no_cand() { return Cand{false, false, 0.0f, 0.0f, 0u}; }
+
+__device__ __forceinline__ Cand closest(const Cand& a, const Cand& b) {  // shader.frag:181-185
+  const bool ta = a.hit && (!b.hit || a.dist < b.dist);
+  return Cand{ta ? a.hit : b.hit, ta ? a.flip : b.flip, ta ? a.dist : b.dist, ta ? a.sdist : b.sdist,
+              ta ? a.id : b.id};
+}
+
+// sphere_intersection without the normal (shader.frag:197-217). The early returns matter on a GPU:
+// when no lane of the wave needs the rest, the wave skips it (s_cbranch_execz).
+__device__ __forceinline__ Cand sphere_cand(V4 center, float r, const DivC& dc, const Ray& ray, bool outer,
+                                            uint32_t id) {
+  V4 vec_po = sub(center, ray.point);
+  const float len_po = length(vec_po);
+  float cos_opa = 0.0f;
+  if (!(len_po < SMALL_F)) {
+    const float dot_pord = dot(vec_po, ray.drct);
+    if (len_po >= r && dot_pord < 0.0f) return no_cand();
+    cos_opa = dot_pord / len_po;
+    cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
+    cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
+  }
+  const float angle_opa = acos_(cos_opa);
+  const float sin_oap = div_c(len_po * sin_(angle_opa), dc);
+  if (sin_oap >= 1.0f) return no_cand();
+  float angle_oap = asin_(sin_oap);
+  const bool flip = outer && len_po > r;
+  if (flip) angle_oap = PI_F - angle_oap;
+  const float angle_aop = PI_F - angle_opa - angle_oap;
+  const float dist = __builtin_sqrtf(r * r + len_po * len_po - 2.0f * r * len_po * cos_(angle_aop));
+  return Cand{true, flip, dist, dist, id};
+}
+
+// Sphere-core shared by the outer=true/false variants of one cylinder face pair.
+struct SphereCore2 {
+  bool miss;
+  float len_po, angle_opa, angle_oap;
+};
+__device__ __forceinline__ SphereCore2 sphere_core2(V4 center, float r, const DivC& dc, const Ray& ray) {
+  SphereCore2 c;
+  V4 vec_po = sub(center, ray.point);
+  c.len_po = length(vec_po);
+  float cos_opa = 0.0f;
+  c.miss = false;
+  c.angle_opa = 0.0f;
+  c.angle_oap = 0.0f;
+  if (!(c.len_po < SMALL_F)) {
+    const float dot_pord = dot(vec_po, ray.drct);
+    c.miss = c.len_po >= r && dot_pord < 0.0f;
+    cos_opa = dot_pord / c.len_po;
+    cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
+    cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
+  }
+  if (c.miss) return c;
+  c.angle_opa = acos_(cos_opa);
+  const float sin_oap = div_c(c.len_po * sin_(c.angle_opa), dc);
+  c.miss = sin_oap >= 1.0f;
+  if (c.miss) return c;
+  c.angle_oap = asin_(sin_oap);
+  return c;
+}
+__device__ __forceinline__ void sphere_dist2(const SphereCore2& c, float r, float& d_outer, bool& flip_outer,
+                                             float& d_inner) {
+  // outer = true
+  flip_outer = c.len_po > r;
+  {
+    const float oap = flip_outer ? PI_F - c.angle_oap : c.angle_oap;
+    const float aop = PI_F - c.angle_opa - oap;
+    d_outer = __builtin_sqrtf(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(aop));
+  }
+  if (flip_outer) {  // outer = false never flips
+    const float aop = PI_F - c.angle_opa - c.angle_oap;
+    d_inner = __builtin_sqrtf(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(aop));
+  } else {
+    d_inner = d_outer;  // identical op sequence when no flip
+  }
+}
+
+__device__ __forceinline__ Cand space_cand(const rt4_scene_desc* __restrict__ S, int i, const Ray& ray) {  // :231-239
+  const rt4_space& s = S->spaces[i];
+  const V4 sn = ld4(s.norm);
+  const float dot_vn = dot(sub(ld4(s.point), ray.point), sn);
+  const float sgn = dot_vn > 0.0f ? 1.0f : (dot_vn < 0.0f ? -1.0f : 0.0f);
+  const float cos_dh = dot(mul(sn, sgn), ray.drct);
+  Cand c{true, sgn < 0.0f, 0.0f, 0.0f, make_id(ID_SPACE, static_cast<uint32_t>(i))};
+  if (cos_dh < SMALL_F) return no_cand();
+  c.dist = __builtin_fabsf(dot_vn) / cos_dh;
+  return c;
+}
+
+// 2-axis cylinder candidate (shader.frag:251-267); p = the ray projected onto its 2-plane
+__device__ __forceinline__ Cand cyl_cand(const CylProj& p, V4 cp, float r, const DivC& dc, bool outer, uint32_t id) {
+  if (p.miss) return no_cand();
+  Cand c = sphere_cand(cp, r, dc, p.r12, outer, id);
+  c.dist = c.dist / p.len;  // inter.dist /= drct_in_plane_length (:265)
+  return c;
+}
+
+// dist_to_axes_plane(..)^2 without the sqrt (shader.frag:270-275)
+__device__ __forceinline__ float axes_dist_sq(float dist, const Ray& ray, V4 cp, V4 a1, V4 a2) {
+  const V4 p = mad(ray.drct, dist, ray.point);
+  const V4 p1 = point_in_space(p, cp, a1);
+  const V4 p12 = point_in_space(p1, cp, a2);
+  const V4 v = sub(cp, p12);
+  return dot(v, v);
+}
+
+__device__ __forceinline__ Cand union_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                           int i, const Ray& ray) {  // :284-294
+  const rt4_cylinders_union& u = S->unions[i];
+  const V4 p1 = ld4(u.cylinder1.point), a11 = ld4(u.cylinder1.axis1), a12 = ld4(u.cylinder1.axis2);
+  const V4 p2 = ld4(u.cylinder2.point), a21 = ld4(u.cylinder2.axis1), a22 = ld4(u.cylinder2.axis2);
+  const float gt = X->union_gt[i];
+  Cand c1 = cyl_cand(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], true,
+                     make_id(ID_UNION, static_cast<uint32_t>(2 * i)));
+  if (c1.hit && axes_dist_sq(c1.dist, ray, p2, a21, a22) > gt) c1.hit = false;
+  Cand c2 = cyl_cand(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], true,
+                     make_id(ID_UNION, static_cast<uint32_t>(2 * i + 1)));
+  if (c2.hit && axes_dist_sq(c2.dist, ray, p1, a11, a12) > gt) c2.hit = false;
+  return closest(c1, c2);
+}
+
+// Four faces of one axes pair of a tiger: cylinders (cp, a1, a2) with radii r_in, r_out, each with
+// outer = true/false, kept iff the other pair's axes distance d satisfies lt <= d^2 <= gt.
+__device__ __forceinline__ Cand tiger_pair(V4 cp, V4 a1, V4 a2, float r_in, float r_out, const DivC& dc_in,
+                                           const DivC& dc_out, V4 op, V4 oa1, V4 oa2, float gt, float lt,
+                                           const Ray& ray, uint32_t id_base) {
+  const CylProj p = cyl_project(cp, a1, a2, ray);
+  if (p.miss) return no_cand();
+  Cand res;
+  {
+    res = no_cand();
+    const SphereCore2 c = sphere_core2(cp, r_in, dc_in, p.r12);
+    if (!c.miss) {
+      float d_o, d_i;
+      bool f_o;
+      sphere_dist2(c, r_in, d_o, f_o, d_i);
+      Cand c_o{true, f_o, d_o / p.len, d_o, id_base};    // face x11 (outer = true)
+      Cand c_i{true, false, d_i / p.len, d_i, id_base};  // face x12 (outer = false)
+      float q = axes_dist_sq(c_o.dist, ray, op, oa1, oa2);
+      if (q > gt || q < lt) c_o.hit = false;
+      q = axes_dist_sq(c_i.dist, ray, op, oa1, oa2);
+      if (q > gt || q < lt) c_i.hit = false;
+      res = closest(c_o, c_i);
+    }
+  }
+  {
+    const SphereCore2 c = sphere_core2(cp, r_out, dc_out, p.r12);
+    if (!c.miss) {
+      float d_o, d_i;
+      bool f_o;
+      sphere_dist2(c, r_out, d_o, f_o, d_i);
+      Cand c_o{true, f_o, d_o / p.len, d_o, id_base + 1};   // face x21
+      Cand c_i{true, false, d_i / p.len, d_i, id_base + 1};  // face x22
+      float q = axes_dist_sq(c_o.dist, ray, op, oa1, oa2);
+      if (q > gt || q < lt) c_o.hit = false;
+      q = axes_dist_sq(c_i.dist, ray, op, oa1, oa2);
+      if (q > gt || q < lt) c_i.hit = false;
+      res = closest(res, closest(c_o, c_i));
+    }
+  }
+  return res;
+}
+
+__device__ __forceinline__ Cand tiger_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                           int i, const Ray& ray) {  // :327-341
+  const rt4_tiger& t = S->tigers[i];
+  const V4 pA = ld4(t.inner_cyl1.point), a1 = ld4(t.inner_cyl1.axis1), a2 = ld4(t.inner_cyl1.axis2);
+  const V4 pB = ld4(t.inner_cyl2.point), a3 = ld4(t.inner_cyl2.axis1), a4 = ld4(t.inner_cyl2.axis2);
+  const uint32_t base = make_id(ID_TIGER, static_cast<uint32_t>(4 * i));
+  const Cand lo = tiger_pair(pA, a1, a2, t.inner_cyl1.r, t.outer_cyl1.r, X->tiger_r[i][0], X->tiger_r[i][1], pB, a3,
+                             a4, X->tiger_gt[i][0], X->tiger_lt[i][0], ray, base);
+  const Cand hi = tiger_pair(pB, a3, a4, t.inner_cyl2.r, t.outer_cyl2.r, X->tiger_r[i][2], X->tiger_r[i][3], pA, a1,
+                             a2, X->tiger_gt[i][1], X->tiger_lt[i][1], ray, base + 2);
+  return closest(lo, hi);
+}
+
+__device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uint32_t id) {  // :352-366
+  const V4 cpt = ld4(c.point), cn = ld4(c.norm);
+  const V4 vec_n = neg(cn);
+  const float h = dot(sub(cpt, ray.point), vec_n);
+  const float cos_dn = dot(ray.drct, vec_n);
+  if (h < 0.0f || cos_dn < 0.0f) return no_cand();
+  const float dist = h / cos_dn;
+  const V4 vec_cp = sub(mad(ray.drct, dist, ray.point), cpt);
+  if (__builtin_fabsf(dot(vec_cp, ld4(c.x))) > c.r || __builtin_fabsf(dot(vec_cp, ld4(c.y))) > c.r ||
+      __builtin_fabsf(dot(vec_cp, ld4(c.z))) > c.r)
+    return no_cand();
+  return Cand{true, false, dist, 0.0f, id};
+}
+
+__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, int i, const Ray& ray) {  // :394-400
+  const rt4_hypercube& hc = S->hypercubes[i];
+  Cand res = no_cand();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (!res.hit) res = cube_cand(hc.cubes[k], ray, make_id(ID_CUBE, static_cast<uint32_t>(8 * i + k)));
+  }
+  return res;
+}
+
+template <uint32_t K>
+__device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                          const Ray& ray) {
+  Cand inter = no_cand();
+  if (K & K_SPACES) {
+    const int n = S->n_spaces;
+    for (int i = 0; i < n; i++) inter = closest(space_cand(S, i, ray), inter);
+  }
+  if (K & K_SPHERES) {
+    const int n = S->n_spheres;
+    for (int i = 0; i < n; i++) {
+      const rt4_sphere& sp = S->spheres[i];
+      inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true,
+                                  make_id(ID_SPHERE, static_cast<uint32_t>(i))),
+                      inter);
+    }
+  }
+  if (K & K_CYLINDERS) {
+    const int n = S->n_cylinders;
+    for (int i = 0; i < n; i++) {
+      const rt4_cylinder& c = S->cylinders[i];
+      const V4 cp = ld4(c.point);
+      inter = closest(cyl_cand(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], true,
+                               make_id(ID_CYL, static_cast<uint32_t>(i))),
+                      inter);
+    }
+  }
+  if (K & K_UNION) inter = closest(union_cand(S, X, 0, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, 0, ray), inter);
+  if (K & K_TIGER) inter = closest(tiger_cand(S, X, 0, ray), inter);
+  return inter;
+}
+
+// Normal + material of the winning candidate (per-lane data: vector loads from the scene).
+__device__ __forceinline__ V4 cyl_normal(V4 cp, V4 a1, V4 a2, float r, const DivC& dc, float sdist, bool flip,
+                                         const Ray& ray) {
+  const CylProj p = cyl_project(cp, a1, a2, ray);
+  V4 n = divs_c(sub(cp, mad(p.r12.drct, sdist, p.r12.point)), dc);  // shader.frag:218-219 on the projected ray
+  return flip ? neg(n) : n;
+}
+
+__device__ __forceinline__ Hit resolve(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                       const Ray& ray, const Cand& c) {
+  const uint32_t kind = c.id >> 24, idx = c.id & 0xFFFFFFu;
+  Hit h;
+  h.hit = c.hit;
+  h.dist = c.dist;
+  if (kind == ID_SPACE) {
+    const rt4_space& s = S->spaces[idx];
+    h.norm = neg(mul(ld4(s.norm), c.flip ? -1.0f : 1.0f));
+    h.mat = mat_off(S, s.material);
+  } else if (kind == ID_SPHERE) {
+    const rt4_sphere& s = S->spheres[idx];
+    const V4 center = ld4(s.center);
+    V4 n = divs_c(sub(center, mad(ray.drct, c.sdist, ray.point)), X->sphere_r[idx]);  // :218-219
+    h.norm = c.flip ? neg(n) : n;
+    h.mat = mat_off(S, s.material);
+  } else if (kind == ID_CUBE) {
+    const rt4_cube& cb = S->hypercubes[idx >> 3].cubes[idx & 7];
+    h.norm = ld4(cb.norm);
+    h.mat = mat_off(S, cb.material);
+  } else {
+    const rt4_cylinder* cyl;
+    const DivC* dc;
+    if (kind == ID_CYL) {
+      cyl = &S->cylinders[idx];
+      dc = &X->cyl_r[idx];
+    } else if (kind == ID_UNION) {
+      cyl = (idx & 1) ? &S->unions[idx >> 1].cylinder2 : &S->unions[idx >> 1].cylinder1;
+      dc = &X->union_r[idx >> 1][idx & 1];
+    } else {  // ID_TIGER: idx = tiger*4 + pair*2 + outer_radius
+      const rt4_tiger& t = S->tigers[idx >> 2];
+      const uint32_t f = idx & 3u;
+      cyl = f == 0 ? &t.inner_cyl1 : f == 1 ? &t.outer_cyl1 : f == 2 ? &t.inner_cyl2 : &t.outer_cyl2;
+      dc = &X->tiger_r[idx >> 2][f];
+    }
+    h.norm = cyl_normal(ld4(cyl->point), ld4(cyl->axis1), ld4(cyl->axis2), cyl->r, *dc, c.sdist, c.flip, ray);
+    h.mat = mat_off(S, cyl->material);
+  }
+  return h;
+}
+
+}  // namespace rt4

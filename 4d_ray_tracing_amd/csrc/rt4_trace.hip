@@ -18,12 +18,15 @@
 //     device function replaces the divergent loop by one cached load.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <new>
 
 #include "../../include/rt4.h"
 #include "rt4_device_math.h"
+#include "rt4_fast.h"
 #include "rt4_intersect.h"
 #include "rt4_internal.h"
 
@@ -36,23 +39,43 @@ constexpr unsigned REFILL_MIN = 8;  // refill a wave once this many of its lanes
 constexpr uint32_t GENERIC = 0xFFFFFFFFu;
 constexpr int QUEUE_SLOTS = 64;     // rotating per-launch queue words (see rt4_render_device)
 
+// find_intersection front-ends: the generic group loop returns a full Hit; the specialised path
+// returns a candidate whose normal/material are resolved only on a hit (rt4_fast.h).
 template <uint32_t K>
-__device__ __forceinline__ Hit find_intersection(const rt4_scene_desc* __restrict__ S, const Ray& ray) {
-  if constexpr (K == GENERIC)
+struct Finder {
+  using R = Cand;
+  static __device__ __forceinline__ Cand find(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                              const Ray& ray) {
+    return find_cand<K>(S, X, ray);
+  }
+  static __device__ __forceinline__ Hit resolve(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                                const Ray& ray, const Cand& c) {
+    return rt4::resolve(S, X, ray, c);
+  }
+};
+template <>
+struct Finder<GENERIC> {
+  using R = Hit;
+  static __device__ __forceinline__ Hit find(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__,
+                                             const Ray& ray) {
     return find_intersection_generic(S, ray);
-  else
-    return find_intersection_spec<K>(S, ray);
-}
+  }
+  static __device__ __forceinline__ Hit resolve(const rt4_scene_desc* __restrict__, const SceneAux* __restrict__,
+                                                const Ray&, const Hit& h) {
+    return h;
+  }
+};
 
 // ---------------------------------------------------------------- shading (shader.frag:404-495)
-__device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, V4 drct) {  // :454-468
+__device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                         V4 drct) {  // :454-468
   if (S->final_light_mode == RT4_FINAL_LIGHT_CONSTANT) return ld3(S->final_light_const);
   V3 sky = ld3(S->sky_light);
   V4 sd = ld4(S->sun.drct);
   float deviation = acos_(dot(drct, sd) / length(drct) / length(sd));  // angle(), :45-50
   float ang = S->sun.angular_size;
   if (deviation < ang) {
-    float k = deviation / ang, s = S->sun.sharpness;
+    float k = div_c(deviation, X->sun_ang), s = S->sun.sharpness;
     k = (s * s * k / (1.0f - s * k) + 1.0f) * (1.0f - k);
     float km = 1.0f - k;
     return V3{fmaf_(S->sun.light[0], k, sky.x * km), fmaf_(S->sun.light[1], k, sky.y * km),
@@ -111,7 +134,8 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, float4* __restr
 }
 
 template <uint32_t K, bool LUT>
-__global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S, const KernelArgs a,
+__global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
+                                                        const SceneAux* __restrict__ X, const KernelArgs a,
                                                         float4* __restrict__ frame,
                                                         unsigned long long* __restrict__ counter,
                                                         const float* __restrict__ wlut, unsigned* __restrict__ queue) {
@@ -198,14 +222,15 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
       continue;
     }
     if (active) {
-      Hit h = find_intersection<K>(S, ray);  // :475
+      const typename Finder<K>::R c = Finder<K>::find(S, X, ray);  // :475
       ++n_inter;
       bool end;
-      if (!h.hit) {  // :477-479
-        const V3 fl = final_light(S, ray.drct);
+      if (!c.hit) {  // :477-479
+        const V3 fl = final_light(S, X, ray.drct);
         acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
         end = true;
       } else {
+        const Hit h = Finder<K>::resolve(S, X, ray, c);
         const rt4_material* m = reinterpret_cast<const rt4_material*>(Sb + h.mat);
         const float glow = m->glow, refl = m->refl_prob;
         const V3 c{m->color[0], m->color[1], m->color[2]};
@@ -251,6 +276,21 @@ __global__ void rt4_build_wlut_kernel(float* __restrict__ lut) {
   if (m < (1u << 23)) lut[m] = w_by_volume(__uint_as_float(m | 0x3F800000u) - 1.0f, nullptr);
 }
 
+// Exhaustive check of div_c against the IEEE quotient for every 32-bit numerator pattern.
+__global__ void rt4_verify_div_kernel(float b, float y, unsigned* __restrict__ mismatches) {
+  const DivC c{b, y, 1, 0};
+  unsigned bad = 0;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+    const float x = __uint_as_float(static_cast<uint32_t>(i));
+    const float q1 = x / b;
+    const float q2 = div_c(x, c);
+    const bool same = __float_as_uint(q1) == __float_as_uint(q2) || (q1 != q1 && q2 != q2);
+    bad += same ? 0u : 1u;
+  }
+  if (bad) atomicAdd(mismatches, bad);
+}
+
 __global__ void rt4_eval_kernel(int fn, const float* __restrict__ in, float* __restrict__ out, int32_t* __restrict__ aux,
                                 int64_t n) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -273,12 +313,16 @@ __global__ void rt4_eval_kernel(int fn, const float* __restrict__ in, float* __r
 }
 
 template <uint32_t K>
-__global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const float* __restrict__ rays,
-                                float* __restrict__ out, float* __restrict__ out_color, int64_t n) {
+__global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                const float* __restrict__ rays, float* __restrict__ out,
+                                float* __restrict__ out_color, int64_t n) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const float* r = rays + 8 * t;
-  Hit h = find_intersection<K>(S, Ray{ld4(r), ld4(r + 4)});
+  const Ray ray{ld4(r), ld4(r + 4)};
+  const typename Finder<K>::R c = Finder<K>::find(S, X, ray);
+  Hit h = c.hit ? Finder<K>::resolve(S, X, ray, c) : no_hit();
+  h.dist = c.dist;
   float* o = out + 8 * t;
   o[0] = h.hit ? 1.0f : 0.0f;
   o[1] = h.dist;
@@ -294,8 +338,9 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const floa
 }
 
 // ---------------------------------------------------------------- kernel table
-typedef void (*TraceFn)(const rt4_scene_desc*, const KernelArgs, float4*, unsigned long long*, const float*, unsigned*);
-typedef void (*FindFn)(const rt4_scene_desc*, const float*, float*, float*, int64_t);
+typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, float4*, unsigned long long*,
+                        const float*, unsigned*);
+typedef void (*FindFn)(const rt4_scene_desc*, const SceneAux*, const float*, float*, float*, int64_t);
 
 struct Variant {
   uint32_t shape;
@@ -364,7 +409,10 @@ const Variant& variant_for(uint32_t shape) {
 struct rt4_context {
   int device = 0;
   uint32_t flags = 0;
-  rt4_scene_desc* d_scene = nullptr;
+  rt4_scene_desc* d_scene = nullptr;  // followed by its SceneAux (scene_aux())
+  SceneAux aux{};
+  unsigned* d_scratch = nullptr;      // verification counter
+  std::map<uint32_t, bool> div_ok;   // verified divisors (by bit pattern)
   bool has_scene = false;
   uint32_t shape = GENERIC;
   float* d_wlut = nullptr;
@@ -381,6 +429,84 @@ struct rt4_context {
       return RT4_ERR_HIP;                                                                        \
     }                                                                                            \
   } while (0)
+
+namespace {
+
+constexpr size_t kAuxOffset = (sizeof(rt4_scene_desc) + 255) & ~size_t(255);
+constexpr size_t kSceneBytes = kAuxOffset + sizeof(SceneAux);
+
+const SceneAux* scene_aux(const rt4_context* c) {
+  return reinterpret_cast<const SceneAux*>(reinterpret_cast<const char*>(c->d_scene) + kAuxOffset);
+}
+
+float fbits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+// Largest x >= 0 with RN(sqrt(x)) <= r: then sqrt(x) > r  <=>  x > gt.
+float sqrt_gt_threshold(float r) {
+  uint32_t lo = 0, hi = 0x7F800000u;  // predicate true at lo (sqrt(0) = 0 <= r), false at +inf
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (std::sqrt(fbits(mid)) <= r) lo = mid; else hi = mid;
+  }
+  return fbits(lo);
+}
+// Smallest x >= 0 with RN(sqrt(x)) >= r: then sqrt(x) < r  <=>  x < lt.
+float sqrt_lt_threshold(float r) {
+  if (!(r > 0.0f)) return 0.0f;
+  uint32_t lo = 0, hi = 0x7F800000u;  // false at lo (sqrt(0) < r), true at +inf
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (std::sqrt(fbits(mid)) >= r) hi = mid; else lo = mid;
+  }
+  return fbits(hi);
+}
+
+int make_divc(rt4_context* ctx, float b, DivC* out, char* err, size_t errlen) {
+  DivC d{b, 1.0f / b, 0, 0};
+  uint32_t key;
+  std::memcpy(&key, &b, 4);
+  auto it = ctx->div_ok.find(key);
+  if (it == ctx->div_ok.end()) {
+    bool ok = false;
+    if (std::isfinite(b) && b != 0.0f && std::isfinite(d.y)) {
+      HIP_TRY(hipMemset(ctx->d_scratch, 0, sizeof(unsigned)));
+      hipLaunchKernelGGL(rt4_verify_div_kernel, dim3(65536), dim3(256), 0, 0, b, d.y, ctx->d_scratch);
+      HIP_TRY(hipGetLastError());
+      unsigned bad = 1;
+      HIP_TRY(hipMemcpy(&bad, ctx->d_scratch, sizeof(unsigned), hipMemcpyDeviceToHost));
+      ok = bad == 0;
+    }
+    it = ctx->div_ok.emplace(key, ok).first;
+  }
+  d.fast = it->second ? 1 : 0;
+  *out = d;
+  return RT4_OK;
+}
+
+int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err, size_t errlen) {
+  std::memset(a, 0, sizeof *a);
+  int st = RT4_OK;
+  for (int i = 0; i < s.n_spheres && st == RT4_OK; i++) st = make_divc(ctx, s.spheres[i].r, &a->sphere_r[i], err, errlen);
+  for (int i = 0; i < s.n_cylinders && st == RT4_OK; i++) st = make_divc(ctx, s.cylinders[i].r, &a->cyl_r[i], err, errlen);
+  for (int i = 0; i < s.n_unions && st == RT4_OK; i++) {
+    st = make_divc(ctx, s.unions[i].cylinder1.r, &a->union_r[i][0], err, errlen);
+    if (st == RT4_OK) st = make_divc(ctx, s.unions[i].cylinder2.r, &a->union_r[i][1], err, errlen);
+    a->union_gt[i] = sqrt_gt_threshold(s.unions[i].cylinder2.r);
+  }
+  for (int i = 0; i < s.n_tigers && st == RT4_OK; i++) {
+    const rt4_tiger& t = s.tigers[i];
+    const float rs[4] = {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r};
+    for (int k = 0; k < 4 && st == RT4_OK; k++) st = make_divc(ctx, rs[k], &a->tiger_r[i][k], err, errlen);
+    a->tiger_gt[i][0] = sqrt_gt_threshold(t.outer_cyl2.r);
+    a->tiger_lt[i][0] = sqrt_lt_threshold(t.inner_cyl2.r);
+    a->tiger_gt[i][1] = sqrt_gt_threshold(t.outer_cyl1.r);
+    a->tiger_lt[i][1] = sqrt_lt_threshold(t.inner_cyl1.r);
+  }
+  if (st == RT4_OK) st = make_divc(ctx, s.sun.angular_size, &a->sun_ang, err, errlen);
+  return st;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -399,7 +525,8 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   c->device = device;
   c->flags = flags;
   hipError_t e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
-  if (e == hipSuccess) e = hipMalloc(&c->d_scene, sizeof(rt4_scene_desc));
+  if (e == hipSuccess) e = hipMalloc(&c->d_scene, kSceneBytes);
+  if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess && (flags & RT4_FLAG_SAMPLER_LUT)) {
     e = hipMalloc(&c->d_wlut, sizeof(float) << 23);
@@ -424,6 +551,7 @@ void rt4_context_destroy(rt4_context* ctx) {
   if (ctx->d_scene) (void)hipFree(ctx->d_scene);
   if (ctx->d_wlut) (void)hipFree(ctx->d_wlut);
   if (ctx->d_queue) (void)hipFree(ctx->d_queue);
+  if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
   delete ctx;
 }
 
@@ -432,7 +560,11 @@ int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* e
   int st = rt4_scene_validate(scene, err, errlen);
   if (st != RT4_OK) return st;
   HIP_TRY(hipSetDevice(ctx->device));
+  st = build_aux(ctx, *scene, &ctx->aux, err, errlen);
+  if (st != RT4_OK) return st;
   HIP_TRY(hipMemcpy(ctx->d_scene, scene, sizeof(rt4_scene_desc), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(reinterpret_cast<char*>(ctx->d_scene) + kAuxOffset, &ctx->aux, sizeof(SceneAux),
+                    hipMemcpyHostToDevice));
   ctx->shape = (ctx->flags & RT4_FLAG_GENERIC_KERNEL) ? GENERIC : scene_shape(*scene);
   ctx->has_scene = true;
   return RT4_OK;
@@ -461,7 +593,7 @@ int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region*
   if (blocks < 1) blocks = 1;
   unsigned* q = ctx->d_queue + (ctx->launch_seq++ % QUEUE_SLOTS);
   HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
-  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, a,
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a,
                      reinterpret_cast<float4*>(d_rgba), d_counter, ctx->d_wlut, q);
   HIP_TRY(hipGetLastError());
   return RT4_OK;
@@ -547,7 +679,7 @@ int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out,
   if (e == hipSuccess) e = hipMalloc(&dcol, n * 3 * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(dr, rays, n * 8 * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(variant_for(ctx->shape).find, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, 0, ctx->d_scene,
+    hipLaunchKernelGGL(variant_for(ctx->shape).find, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, 0, ctx->d_scene, scene_aux(ctx),
                        dr, dout, dcol, n);
     e = hipGetLastError();
   }

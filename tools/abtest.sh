@@ -1,0 +1,42 @@
+#!/usr/bin/env bash
+# A/B several builds of librt4.so in one GPU session.
+#   build side (here):  tools/abtest.sh build <name>=<git-rev|WORKTREE> ...
+#   run side (GPU box): tools/abtest.sh run [rounds] [bench args...]
+# Variants live in 4d_ray_tracing_amd/lib/variants/<name>.so; bench.py loads one via RT4_LIB.
+set -eu
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+VDIR=$ROOT/4d_ray_tracing_amd/lib/variants
+cmd=${1:-}; shift || true
+if [ "$cmd" = build ]; then
+  rm -rf "$VDIR"; mkdir -p "$VDIR"
+  for spec in "$@"; do
+    name=${spec%%=*}; rev=${spec#*=}
+    if [ "$rev" = WORKTREE ]; then
+      make -C "$ROOT/4d_ray_tracing_amd/csrc" -s >/dev/null
+      cp "$ROOT/4d_ray_tracing_amd/lib/librt4.so" "$VDIR/$name.so"
+    else
+      tmp=$(mktemp -d)
+      git -C "$ROOT" archive "$rev" 4d_ray_tracing_amd/csrc include | tar -x -C "$tmp"
+      make -C "$tmp/4d_ray_tracing_amd/csrc" -s OUT="$tmp/lib" >/dev/null
+      cp "$tmp/lib/librt4.so" "$VDIR/$name.so"
+      rm -rf "$tmp"
+    fi
+    echo "built $name ($rev)"
+  done
+elif [ "$cmd" = run ]; then
+  rounds=${1:-2}; shift || true
+  args=${*:-"--steps 30 --warmup 3 --no-cpu-baseline"}
+  for r in $(seq 1 "$rounds"); do
+    for so in "$VDIR"/*.so; do
+      name=$(basename "$so" .so)
+      out=$(RT4_LIB=$so timeout -k 10 300 python "$ROOT/bench.py" $args 2>/dev/null | tail -1)
+      python3 - "$name" "$out" <<'PY'
+import json, sys
+d = json.loads(sys.argv[2])
+print(f"{sys.argv[1]:>12s}  {d['value']/1e9:8.2f} G int/s  kernel {d['kernel_ms']:.3f} ms  valu {d['roofline']['frac']*100:5.2f}%  {d['config']['scene']}")
+PY
+    done
+  done
+else
+  echo "usage: $0 build name=rev ... | run [rounds] [bench args]"; exit 2
+fi
