@@ -22,7 +22,30 @@ struct DivC {
   int32_t pad;
 };
 
+// One entry per primitive that can be a hit (flat index = Cand.id): what resolve() needs to build
+// the normal of the winning hit, and its material. Staged into LDS by every workgroup.
+enum PrimKind : int32_t { PK_SPACE = 0, PK_SPHERE = 1, PK_CYLINDER = 2, PK_CUBE = 3 };
+struct PrimEntry {
+  float p[4];     // space.norm | sphere.center | cylinder.point | cube.norm
+  float a1[4];    // cylinder.axis1
+  float a2[4];    // cylinder.axis2
+  float r;        // sphere / cylinder radius (divisor of the normal)
+  float y;        // DivC.y for r
+  int32_t fast;   // DivC.fast for r
+  int32_t kind;   // PrimKind
+  float glow, refl, color[3];  // material (shader.frag:163-167)
+  float pad[3];
+};
+static_assert(sizeof(PrimEntry) == 96, "PrimEntry is 6 x 16 B");
+constexpr int MAX_PRIMS = RT4_MAX_SPACES + RT4_MAX_SPHERES + RT4_MAX_CYLINDERS + 2 * RT4_MAX_UNIONS +
+                          8 * RT4_MAX_HYPERCUBES + 4 * RT4_MAX_TIGERS;
+
 struct SceneAux {
+  // flat primitive ids: spaces, spheres, cylinders, union cylinders (2 per union), cubes (8 per
+  // hypercube), tiger cylinders (inner1, outer1, inner2, outer2 per tiger)
+  int32_t n_prims;
+  int32_t base_sphere, base_cyl, base_union, base_cube, base_tiger;
+  int32_t pad_[2];
   DivC sphere_r[RT4_MAX_SPHERES];
   DivC cyl_r[RT4_MAX_CYLINDERS];
   DivC union_r[RT4_MAX_UNIONS][2];
@@ -31,6 +54,7 @@ struct SceneAux {
   float tiger_gt[RT4_MAX_TIGERS][2];   // [0]: gt(outer_cyl2.r) filters faces 1xx; [1]: gt(outer_cyl1.r) filters 2xx
   float tiger_lt[RT4_MAX_TIGERS][2];   // [0]: lt(inner_cyl2.r);                    [1]: lt(inner_cyl1.r)
   DivC sun_ang;
+  PrimEntry prims[MAX_PRIMS];
 };
 
 }  // namespace rt4

@@ -27,22 +27,12 @@ __device__ __forceinline__ V4 divs_c(V4 a, const DivC& c) {
   return V4{div_c(a.x, c), div_c(a.y, c), div_c(a.z, c), div_c(a.w, c)};
 }
 
-enum : uint32_t {
-  ID_SPACE = 0u,
-  ID_SPHERE = 1u,
-  ID_CYL = 2u,
-  ID_UNION = 3u,   // idx = union*2 + which cylinder
-  ID_CUBE = 4u,    // idx = hypercube*8 + cell
-  ID_TIGER = 5u,   // idx = tiger*4 + (pair*2 + outer_radius)
-};
-__device__ __forceinline__ uint32_t make_id(uint32_t kind, uint32_t idx) { return (kind << 24) | idx; }
-
 struct Cand {
   bool hit;
   bool flip;    // sphere-like: normal negated (outer && len_po > r); space: sign(dot_vn) < 0
   float dist;   // distance along the ray (what closest() compares)
   float sdist;  // cylinder-like: distance inside the projected 2-plane (before /= len)
-  uint32_t id;
+  uint32_t id;  // flat primitive index into SceneAux::prims (rt4_aux.h)
 };
 
 __device__ __forceinline__ Cand no_cand() { return Cand{false, false, 0.0f, 0.0f, 0u}; }
@@ -129,7 +119,7 @@ __device__ __forceinline__ Cand space_cand(const rt4_scene_desc* __restrict__ S,
   const float dot_vn = dot(sub(ld4(s.point), ray.point), sn);
   const float sgn = dot_vn > 0.0f ? 1.0f : (dot_vn < 0.0f ? -1.0f : 0.0f);
   const float cos_dh = dot(mul(sn, sgn), ray.drct);
-  Cand c{true, sgn < 0.0f, 0.0f, 0.0f, make_id(ID_SPACE, static_cast<uint32_t>(i))};
+  Cand c{true, sgn < 0.0f, 0.0f, 0.0f, static_cast<uint32_t>(i)};
   if (cos_dh < SMALL_F) return no_cand();
   c.dist = __builtin_fabsf(dot_vn) / cos_dh;
   return c;
@@ -158,11 +148,10 @@ __device__ __forceinline__ Cand union_cand(const rt4_scene_desc* __restrict__ S,
   const V4 p1 = ld4(u.cylinder1.point), a11 = ld4(u.cylinder1.axis1), a12 = ld4(u.cylinder1.axis2);
   const V4 p2 = ld4(u.cylinder2.point), a21 = ld4(u.cylinder2.axis1), a22 = ld4(u.cylinder2.axis2);
   const float gt = X->union_gt[i];
-  Cand c1 = cyl_cand(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], true,
-                     make_id(ID_UNION, static_cast<uint32_t>(2 * i)));
+  const uint32_t base = static_cast<uint32_t>(X->base_union + 2 * i);
+  Cand c1 = cyl_cand(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], true, base);
   if (c1.hit && axes_dist_sq(c1.dist, ray, p2, a21, a22) > gt) c1.hit = false;
-  Cand c2 = cyl_cand(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], true,
-                     make_id(ID_UNION, static_cast<uint32_t>(2 * i + 1)));
+  Cand c2 = cyl_cand(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], true, base + 1);
   if (c2.hit && axes_dist_sq(c2.dist, ray, p1, a11, a12) > gt) c2.hit = false;
   return closest(c1, c2);
 }
@@ -214,7 +203,7 @@ __device__ __forceinline__ Cand tiger_cand(const rt4_scene_desc* __restrict__ S,
   const rt4_tiger& t = S->tigers[i];
   const V4 pA = ld4(t.inner_cyl1.point), a1 = ld4(t.inner_cyl1.axis1), a2 = ld4(t.inner_cyl1.axis2);
   const V4 pB = ld4(t.inner_cyl2.point), a3 = ld4(t.inner_cyl2.axis1), a4 = ld4(t.inner_cyl2.axis2);
-  const uint32_t base = make_id(ID_TIGER, static_cast<uint32_t>(4 * i));
+  const uint32_t base = static_cast<uint32_t>(X->base_tiger + 4 * i);
   const Cand lo = tiger_pair(pA, a1, a2, t.inner_cyl1.r, t.outer_cyl1.r, X->tiger_r[i][0], X->tiger_r[i][1], pB, a3,
                              a4, X->tiger_gt[i][0], X->tiger_lt[i][0], ray, base);
   const Cand hi = tiger_pair(pB, a3, a4, t.inner_cyl2.r, t.outer_cyl2.r, X->tiger_r[i][2], X->tiger_r[i][3], pA, a1,
@@ -236,12 +225,14 @@ __device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uin
   return Cand{true, false, dist, 0.0f, id};
 }
 
-__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, int i, const Ray& ray) {  // :394-400
+__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                               int i, const Ray& ray) {  // :394-400
   const rt4_hypercube& hc = S->hypercubes[i];
+  const uint32_t base = static_cast<uint32_t>(X->base_cube + 8 * i);
   Cand res = no_cand();
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    if (!res.hit) res = cube_cand(hc.cubes[k], ray, make_id(ID_CUBE, static_cast<uint32_t>(8 * i + k)));
+    if (!res.hit) res = cube_cand(hc.cubes[k], ray, base + k);
   }
   return res;
 }
@@ -259,7 +250,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
     for (int i = 0; i < n; i++) {
       const rt4_sphere& sp = S->spheres[i];
       inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true,
-                                  make_id(ID_SPHERE, static_cast<uint32_t>(i))),
+                                  static_cast<uint32_t>(X->base_sphere + i)),
                       inter);
     }
   }
@@ -269,12 +260,12 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
       const rt4_cylinder& c = S->cylinders[i];
       const V4 cp = ld4(c.point);
       inter = closest(cyl_cand(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], true,
-                               make_id(ID_CYL, static_cast<uint32_t>(i))),
+                               static_cast<uint32_t>(X->base_cyl + i)),
                       inter);
     }
   }
   if (K & K_UNION) inter = closest(union_cand(S, X, 0, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, 0, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, X, 0, ray), inter);
   if (K & K_TIGER) inter = closest(tiger_cand(S, X, 0, ray), inter);
   return inter;
 }
@@ -287,43 +278,26 @@ __device__ __forceinline__ V4 cyl_normal(V4 cp, V4 a1, V4 a2, float r, const Div
   return flip ? neg(n) : n;
 }
 
-__device__ __forceinline__ Hit resolve(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                       const Ray& ray, const Cand& c) {
-  const uint32_t kind = c.id >> 24, idx = c.id & 0xFFFFFFu;
+// Normal of the winning candidate from its LDS primitive entry; Hit.mat = the flat primitive index.
+// Only the kinds the scene shape K can produce are compiled in.
+template <uint32_t K>
+__device__ __forceinline__ Hit resolve(const PrimEntry* P, const Ray& ray, const Cand& c) {
+  const PrimEntry& e = P[c.id];
+  const int kind = e.kind;
   Hit h;
   h.hit = c.hit;
   h.dist = c.dist;
-  if (kind == ID_SPACE) {
-    const rt4_space& s = S->spaces[idx];
-    h.norm = neg(mul(ld4(s.norm), c.flip ? -1.0f : 1.0f));
-    h.mat = mat_off(S, s.material);
-  } else if (kind == ID_SPHERE) {
-    const rt4_sphere& s = S->spheres[idx];
-    const V4 center = ld4(s.center);
-    V4 n = divs_c(sub(center, mad(ray.drct, c.sdist, ray.point)), X->sphere_r[idx]);  // :218-219
+  h.mat = static_cast<int>(c.id);
+  h.norm = ld4(e.p);  // PK_CUBE: the cell's space.norm (shader.frag:365)
+  if ((K & K_SPACES) && kind == PK_SPACE) {
+    h.norm = neg(mul(ld4(e.p), c.flip ? -1.0f : 1.0f));  // -drct_h (shader.frag:234,238)
+  } else if ((K & K_SPHERES) && kind == PK_SPHERE) {
+    const DivC dc{e.r, e.y, e.fast, 0};
+    const V4 n = divs_c(sub(ld4(e.p), mad(ray.drct, c.sdist, ray.point)), dc);  // :218-219
     h.norm = c.flip ? neg(n) : n;
-    h.mat = mat_off(S, s.material);
-  } else if (kind == ID_CUBE) {
-    const rt4_cube& cb = S->hypercubes[idx >> 3].cubes[idx & 7];
-    h.norm = ld4(cb.norm);
-    h.mat = mat_off(S, cb.material);
-  } else {
-    const rt4_cylinder* cyl;
-    const DivC* dc;
-    if (kind == ID_CYL) {
-      cyl = &S->cylinders[idx];
-      dc = &X->cyl_r[idx];
-    } else if (kind == ID_UNION) {
-      cyl = (idx & 1) ? &S->unions[idx >> 1].cylinder2 : &S->unions[idx >> 1].cylinder1;
-      dc = &X->union_r[idx >> 1][idx & 1];
-    } else {  // ID_TIGER: idx = tiger*4 + pair*2 + outer_radius
-      const rt4_tiger& t = S->tigers[idx >> 2];
-      const uint32_t f = idx & 3u;
-      cyl = f == 0 ? &t.inner_cyl1 : f == 1 ? &t.outer_cyl1 : f == 2 ? &t.inner_cyl2 : &t.outer_cyl2;
-      dc = &X->tiger_r[idx >> 2][f];
-    }
-    h.norm = cyl_normal(ld4(cyl->point), ld4(cyl->axis1), ld4(cyl->axis2), cyl->r, *dc, c.sdist, c.flip, ray);
-    h.mat = mat_off(S, cyl->material);
+  } else if ((K & (K_CYLINDERS | K_UNION | K_TIGER)) && kind == PK_CYLINDER) {
+    const DivC dc{e.r, e.y, e.fast, 0};
+    h.norm = cyl_normal(ld4(e.p), ld4(e.a1), ld4(e.a2), e.r, dc, c.sdist, c.flip, ray);
   }
   return h;
 }

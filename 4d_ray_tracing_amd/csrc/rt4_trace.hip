@@ -48,9 +48,15 @@ struct Finder {
                                               const Ray& ray) {
     return find_cand<K>(S, X, ray);
   }
-  static __device__ __forceinline__ Hit resolve(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                                const Ray& ray, const Cand& c) {
-    return rt4::resolve(S, X, ray, c);
+  static __device__ __forceinline__ Hit resolve(const PrimEntry* P, const Ray& ray, const Cand& c) {
+    return rt4::resolve<K>(P, ray, c);
+  }
+  static __device__ __forceinline__ void material(const rt4_scene_desc* __restrict__, const PrimEntry* P, const Hit& h,
+                                                  float& glow, float& refl, V3& color) {
+    const PrimEntry& e = P[h.mat];
+    glow = e.glow;
+    refl = e.refl;
+    color = V3{e.color[0], e.color[1], e.color[2]};
   }
 };
 template <>
@@ -60,9 +66,13 @@ struct Finder<GENERIC> {
                                              const Ray& ray) {
     return find_intersection_generic(S, ray);
   }
-  static __device__ __forceinline__ Hit resolve(const rt4_scene_desc* __restrict__, const SceneAux* __restrict__,
-                                                const Ray&, const Hit& h) {
-    return h;
+  static __device__ __forceinline__ Hit resolve(const PrimEntry*, const Ray&, const Hit& h) { return h; }
+  static __device__ __forceinline__ void material(const rt4_scene_desc* __restrict__ S, const PrimEntry*, const Hit& h,
+                                                  float& glow, float& refl, V3& color) {
+    const rt4_material* m = reinterpret_cast<const rt4_material*>(reinterpret_cast<const char*>(S) + h.mat);
+    glow = m->glow;
+    refl = m->refl_prob;
+    color = V3{m->color[0], m->color[1], m->color[2]};
   }
 };
 
@@ -147,7 +157,15 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
   const float indent = a.u.small_indent;
   const int R = a.u.reflections_amount, NS = a.u.samples;
   const uint32_t useed = static_cast<uint32_t>(a.u.seed);
-  const char* Sb = reinterpret_cast<const char*>(S);
+  // the primitive table (normals + materials of hits) is read per lane: stage it in LDS once
+  __shared__ float4 lds_prims[K == GENERIC ? 1 : MAX_PRIMS * 6];
+  if constexpr (K != GENERIC) {
+    const float4* src = reinterpret_cast<const float4*>(X->prims);
+    const int n4 = X->n_prims * 6;
+    for (int t = threadIdx.x; t < n4; t += blockDim.x) lds_prims[t] = src[t];
+    __syncthreads();
+  }
+  const PrimEntry* P = reinterpret_cast<const PrimEntry*>(lds_prims);
 
   unsigned b_next = 0, b_end = 0;  // wave-uniform: unclaimed part of the current batch
   bool exhausted = false;
@@ -230,10 +248,11 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
         acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
         end = true;
       } else {
-        const Hit h = Finder<K>::resolve(S, X, ray, c);
-        const rt4_material* m = reinterpret_cast<const rt4_material*>(Sb + h.mat);
-        const float glow = m->glow, refl = m->refl_prob;
-        const V3 c{m->color[0], m->color[1], m->color[2]};
+        const Hit h = Finder<K>::resolve(P, ray, c);
+        float glow, refl;
+        V3 col;
+        Finder<K>::material(S, P, h, glow, refl, col);
+        const V3 c = col;
         acc = V3{fmaf_(c.x * glow, T.x, acc.x), fmaf_(c.y * glow, T.y, acc.y), fmaf_(c.z * glow, T.z, acc.z)};  // :481
         T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
         ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                  // :485
@@ -321,16 +340,18 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const Scen
   const float* r = rays + 8 * t;
   const Ray ray{ld4(r), ld4(r + 4)};
   const typename Finder<K>::R c = Finder<K>::find(S, X, ray);
-  Hit h = c.hit ? Finder<K>::resolve(S, X, ray, c) : no_hit();
+  Hit h = c.hit ? Finder<K>::resolve(X->prims, ray, c) : no_hit();
   h.dist = c.dist;
   float* o = out + 8 * t;
   o[0] = h.hit ? 1.0f : 0.0f;
   o[1] = h.dist;
   o[2] = h.norm.x; o[3] = h.norm.y; o[4] = h.norm.z; o[5] = h.norm.w;
   if (h.hit) {
-    const rt4_material* m = reinterpret_cast<const rt4_material*>(reinterpret_cast<const char*>(S) + h.mat);
-    o[6] = m->glow; o[7] = m->refl_prob;
-    out_color[3 * t] = m->color[0]; out_color[3 * t + 1] = m->color[1]; out_color[3 * t + 2] = m->color[2];
+    float glow, refl;
+    V3 col;
+    Finder<K>::material(S, X->prims, h, glow, refl, col);
+    o[6] = glow; o[7] = refl;
+    out_color[3 * t] = col.x; out_color[3 * t + 1] = col.y; out_color[3 * t + 2] = col.z;
   } else {
     o[6] = 0.0f; o[7] = 0.0f;
     out_color[3 * t] = 0.0f; out_color[3 * t + 1] = 0.0f; out_color[3 * t + 2] = 0.0f;
@@ -503,7 +524,52 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     a->tiger_lt[i][1] = sqrt_lt_threshold(t.inner_cyl1.r);
   }
   if (st == RT4_OK) st = make_divc(ctx, s.sun.angular_size, &a->sun_ang, err, errlen);
-  return st;
+  if (st != RT4_OK) return st;
+  // flat primitive table (rt4_aux.h)
+  int n = 0;
+  auto add = [&](int kind, const float* p, const float* a1, const float* a2, float r, const DivC& dc,
+                 const rt4_material& m) {
+    PrimEntry& e = a->prims[n++];
+    std::memcpy(e.p, p, sizeof e.p);
+    if (a1) std::memcpy(e.a1, a1, sizeof e.a1);
+    if (a2) std::memcpy(e.a2, a2, sizeof e.a2);
+    e.r = r;
+    e.y = dc.y;
+    e.fast = dc.fast;
+    e.kind = kind;
+    e.glow = m.glow;
+    e.refl = m.refl_prob;
+    std::memcpy(e.color, m.color, sizeof e.color);
+  };
+  const DivC none{0.0f, 0.0f, 0, 0};
+  for (int i = 0; i < s.n_spaces; i++) add(PK_SPACE, s.spaces[i].norm, nullptr, nullptr, 0.0f, none, s.spaces[i].material);
+  a->base_sphere = n;
+  for (int i = 0; i < s.n_spheres; i++)
+    add(PK_SPHERE, s.spheres[i].center, nullptr, nullptr, s.spheres[i].r, a->sphere_r[i], s.spheres[i].material);
+  a->base_cyl = n;
+  for (int i = 0; i < s.n_cylinders; i++) {
+    const rt4_cylinder& c = s.cylinders[i];
+    add(PK_CYLINDER, c.point, c.axis1, c.axis2, c.r, a->cyl_r[i], c.material);
+  }
+  a->base_union = n;
+  for (int i = 0; i < s.n_unions; i++) {
+    const rt4_cylinder* cs[2] = {&s.unions[i].cylinder1, &s.unions[i].cylinder2};
+    for (int k = 0; k < 2; k++) add(PK_CYLINDER, cs[k]->point, cs[k]->axis1, cs[k]->axis2, cs[k]->r, a->union_r[i][k], cs[k]->material);
+  }
+  a->base_cube = n;
+  for (int i = 0; i < s.n_hypercubes; i++)
+    for (int k = 0; k < 8; k++) {
+      const rt4_cube& c = s.hypercubes[i].cubes[k];
+      add(PK_CUBE, c.norm, nullptr, nullptr, 0.0f, none, c.material);
+    }
+  a->base_tiger = n;
+  for (int i = 0; i < s.n_tigers; i++) {
+    const rt4_tiger& t = s.tigers[i];
+    const rt4_cylinder* cs[4] = {&t.inner_cyl1, &t.outer_cyl1, &t.inner_cyl2, &t.outer_cyl2};
+    for (int k = 0; k < 4; k++) add(PK_CYLINDER, cs[k]->point, cs[k]->axis1, cs[k]->axis2, cs[k]->r, a->tiger_r[i][k], cs[k]->material);
+  }
+  a->n_prims = n;
+  return RT4_OK;
 }
 
 }  // namespace
