@@ -300,6 +300,10 @@ def make_uniforms(width: int, height: int, samples: int, reflections: int, seed:
     return u
 
 
+BUILTIN_SCENES = ("sphere", "room", "tiger", "cylinder4d", "hypercube")
+SCENES_DIR = os.path.join(os.path.dirname(_HERE), "scenes")
+
+
 class Scene:
     """A parsed scene (rt4_scene_desc)."""
 
@@ -327,6 +331,14 @@ class Scene:
         raw = text.encode("utf-8")
         _check(lib.rt4_scene_parse_frag(raw, len(raw), byref(d), err, len(err)), err)
         return cls(d)
+
+    @classmethod
+    def named(cls, name: str) -> "Scene":
+        """A builtin reference scene, or scenes/<name>.frag of this repository, or a path to a .frag file."""
+        if name in BUILTIN_SCENES:
+            return cls.builtin(name)
+        path = name if name.endswith(".frag") else os.path.join(SCENES_DIR, name + ".frag")
+        return cls.load_frag(path)
 
     def to_bytes(self) -> bytes:
         return bytes(self.desc)

@@ -106,7 +106,7 @@ def main():
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
 
     plan = shard.make_plan(args.width, args.height, world, band=8)
-    scene = rt4.Scene.builtin(args.scene)
+    scene = rt4.Scene.named(args.scene)
     flags = 0 if args.no_lut else rt4.FLAG_SAMPLER_LUT
     tracer = rt4.Tracer(device=local_rank, flags=flags, scene=scene)
     u = rt4.make_uniforms(plan.width, plan.height, samples=args.spp, reflections=args.bounces, seed=args.seed)

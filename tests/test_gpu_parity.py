@@ -12,7 +12,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["sphere", "room", "tiger", "cylinder4d", "hypercube"]
+SCENES = ["sphere", "room", "tiger", "cylinder4d", "hypercube", "tiger_two_mirrors", "all_primitives"]
+REF_SCENES = SCENES[:5]
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
@@ -78,7 +79,7 @@ def random_rays(n, seed):
 @pytest.mark.parametrize("name", SCENES)
 @pytest.mark.parametrize("generic", [False, True])
 def test_find_intersection_bitwise(rt4, oracle, name, generic):
-    scene = rt4.Scene.builtin(name)
+    scene = rt4.Scene.named(name)
     t = rt4.Tracer(device=0, scene=scene, flags=rt4.FLAG_GENERIC_KERNEL if generic else 0)
     try:
         rays = random_rays(100000, 1000 + SCENES.index(name))
@@ -110,7 +111,7 @@ def test_render_bitwise_small(rt4, oracle, name, flags):
     u = rt4.make_uniforms(96, 60, samples=4, reflections=4, seed=777)
     reg = rt4.region(96, 60)
     f = {"lut": rt4.FLAG_SAMPLER_LUT, "inline": 0, "generic": rt4.FLAG_GENERIC_KERNEL}[flags]
-    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin(name), u, reg, flags=f)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.named(name), u, reg, flags=f)
     assert ng == nc
     assert_bits(fg, fc, f"{name} image")
 
@@ -119,7 +120,7 @@ def test_render_bitwise_config2_rows(rt4, oracle):
     """BASELINE config 2 (sphere, 1920x1080, 16 spp, 8 bounces, seed 12345) on every 32nd row."""
     u = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
     reg = rt4.region(1920, 34, y0=5, band_rows=1, band_step=32)
-    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin("sphere"), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.named("sphere"), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
     assert ng == nc
     assert_bits(fg, fc, "config2 rows")
 
@@ -128,7 +129,7 @@ def test_render_bitwise_config3_rows(rt4, oracle):
     """BASELINE config 3 (hypercube, 1920x1080, 16 spp, 8 bounces) on every 64th row."""
     u = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
     reg = rt4.region(1920, 17, y0=11, band_rows=1, band_step=64)
-    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin("hypercube"), u, reg)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.named("hypercube"), u, reg)
     assert ng == nc
     assert_bits(fg, fc, "config3 rows")
 
@@ -138,7 +139,7 @@ def test_progressive_blend(rt4, oracle):
     u = rt4.make_uniforms(64, 40, samples=2, reflections=3, seed=99, part=1.0 / 3.0)
     reg = rt4.region(64, 40)
     old = np.random.default_rng(5).random((40, 64, 4), dtype=np.float32)
-    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.builtin("tiger"), u, reg, old=old)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.named("tiger"), u, reg, old=old)
     assert ng == nc
     assert_bits(fg, fc, "progressive")
 
@@ -146,7 +147,7 @@ def test_progressive_blend(rt4, oracle):
 def test_banded_regions_tile_the_image(rt4):
     """Pixel-tile sharding: two interleaved band sets reproduce the full image bit for bit."""
     u = rt4.make_uniforms(80, 64, samples=2, reflections=3, seed=4242)
-    scene = rt4.Scene.builtin("cylinder4d")
+    scene = rt4.Scene.named("cylinder4d")
     t = rt4.Tracer(device=0, scene=scene)
     try:
         full = np.zeros((64, 80, 4), np.float32)
@@ -166,13 +167,13 @@ def test_banded_regions_tile_the_image(rt4):
     assert_bits(rebuilt, full, "banded")
 
 
-@pytest.mark.parametrize("name", SCENES)
+@pytest.mark.parametrize("name", REF_SCENES)
 def test_golden_images(rt4, name):
     """GPU output against the committed oracle images (tests/golden/make_golden.py)."""
     meta = json.load(open(os.path.join(GOLDEN, "images.json")))[name]
     u = rt4.make_uniforms(meta["width"], meta["height"], samples=meta["samples"], reflections=meta["reflections"],
                           seed=meta["seed"])
-    t = rt4.Tracer(device=0, scene=rt4.Scene.builtin(name))
+    t = rt4.Tracer(device=0, scene=rt4.Scene.named(name))
     try:
         f = np.zeros((meta["height"], meta["width"], 4), np.float32)
         n = t.render_host(u, rt4.region(meta["width"], meta["height"]), f)
