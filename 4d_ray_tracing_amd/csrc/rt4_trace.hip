@@ -34,10 +34,37 @@ using namespace rt4;
 
 namespace {
 
-constexpr unsigned BATCH = 64;      // pixels per queue claim: one 8x8 tile
-constexpr unsigned REFILL_MIN = 8;  // refill a wave once this many of its lanes are idle
+#ifndef RT4_REFILL_MIN
+#define RT4_REFILL_MIN 8
+#endif
+#ifndef RT4_WAVES_PER_SIMD
+#define RT4_WAVES_PER_SIMD 1
+#endif
+constexpr unsigned BATCH = 64;                   // pixels per queue claim: one 8x8 tile
+constexpr unsigned REFILL_MIN = RT4_REFILL_MIN;  // refill a wave once this many of its lanes are idle
 constexpr uint32_t GENERIC = 0xFFFFFFFFu;
 constexpr int QUEUE_SLOTS = 64;     // rotating per-launch queue words (see rt4_render_device)
+
+// Diagnostic build only (-DRT4_STAMPS, never shipped): s_memtime stamps accumulate per-wave cycles
+// per loop phase into counter[1..6] (refill, find, miss, resolve, diffuse, total). Read the shares,
+// not the run time: the stamps' own waits change the schedule (cdna_hip_programming.md §7).
+#ifdef RT4_STAMPS
+#define RT4_STAMP(var)                          \
+  do {                                          \
+    __builtin_amdgcn_sched_barrier(0);          \
+    var = __builtin_amdgcn_s_memtime();         \
+    __builtin_amdgcn_sched_barrier(0);          \
+  } while (0)
+#define RT4_ACC(slot, t0)                                   \
+  do {                                                      \
+    unsigned long long t1_;                                 \
+    RT4_STAMP(t1_);                                         \
+    st[slot] += t1_ - (t0);                                 \
+  } while (0)
+#else
+#define RT4_STAMP(var) (void)0
+#define RT4_ACC(slot, t0) (void)0
+#endif
 
 // find_intersection front-ends: the generic group loop returns a full Hit; the specialised path
 // returns a candidate whose normal/material are resolved only on a hit (rt4_fast.h).
@@ -144,7 +171,7 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, float4* __restr
 }
 
 template <uint32_t K, bool LUT>
-__global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
+__global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         float4* __restrict__ frame,
                                                         unsigned long long* __restrict__ counter,
@@ -178,7 +205,12 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
   int s = 0, b = 0;
   uint32_t n_inter = 0;
 
+#ifdef RT4_STAMPS
+  unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;
+  RT4_STAMP(t_loop0);
+#endif
   while (true) {
+    RT4_STAMP(t_ph);
     if (!exhausted) {
       const unsigned long long idle = __ballot(!active);
       if (static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN) {
@@ -235,23 +267,30 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
         }
       }
     }
+    RT4_ACC(0, t_ph);
     if (!__any(active)) {
       if (exhausted) break;
       continue;
     }
     if (active) {
+      RT4_STAMP(t_ph);
       const typename Finder<K>::R c = Finder<K>::find(S, X, ray);  // :475
+      RT4_ACC(1, t_ph);
       ++n_inter;
       bool end;
       if (!c.hit) {  // :477-479
+        RT4_STAMP(t_ph);
         const V3 fl = final_light(S, X, ray.drct);
+        RT4_ACC(2, t_ph);
         acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
         end = true;
       } else {
+        RT4_STAMP(t_ph);
         const Hit h = Finder<K>::resolve(P, ray, c);
         float glow, refl;
         V3 col;
         Finder<K>::material(S, P, h, glow, refl, col);
+        RT4_ACC(3, t_ph);
         const V3 c = col;
         acc = V3{fmaf_(c.x * glow, T.x, acc.x), fmaf_(c.y * glow, T.y, acc.y), fmaf_(c.z * glow, T.z, acc.z)};  // :481
         T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
@@ -260,7 +299,9 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
           const float dn = dot(h.norm, ray.drct);
           ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
         } else {  // :491 redirect(rand_drct(), norm)
+          RT4_STAMP(t_ph);
           const V4 v = rand_drct<LUT>(rng, wlut);
+          RT4_ACC(4, t_ph);
           const float dv = dot(v, h.norm);
           ray.drct = dv >= 0.0f ? v : mad(h.norm, -(2.0f * dv), v);
         }
@@ -282,6 +323,11 @@ __global__ __launch_bounds__(256) void rt4_trace_kernel(const rt4_scene_desc* __
     }
   }
   if (pending) write_pixel(a, frame, pj, pi, light);
+#ifdef RT4_STAMPS
+  RT4_ACC(5, t_loop0);
+  if (counter && lane == 0)
+    for (int q = 0; q < 6; q++) atomicAdd(counter + 1 + q, st[q]);
+#endif
 
   if (counter) {  // wave-level sum, one atomic per wave
     unsigned long long v = n_inter;

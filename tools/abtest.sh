@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # A/B several builds of librt4.so in one GPU session.
-#   build side (here):  tools/abtest.sh build <name>=<git-rev|WORKTREE> ...
+#   build side (here):  tools/abtest.sh build <name>=<git-rev|WORKTREE[:-DFLAG=1 ...]> ...
 #   run side (GPU box): tools/abtest.sh run [rounds] [bench args...]
 # Variants live in 4d_ray_tracing_amd/lib/variants/<name>.so; bench.py loads one via RT4_LIB.
 set -eu
@@ -11,9 +11,13 @@ if [ "$cmd" = build ]; then
   rm -rf "$VDIR"; mkdir -p "$VDIR"
   for spec in "$@"; do
     name=${spec%%=*}; rev=${spec#*=}
+    flags=""
+    case "$rev" in WORKTREE:*) flags=${rev#WORKTREE:}; rev=WORKTREE;; esac
     if [ "$rev" = WORKTREE ]; then
-      make -C "$ROOT/4d_ray_tracing_amd/csrc" -s >/dev/null
-      cp "$ROOT/4d_ray_tracing_amd/lib/librt4.so" "$VDIR/$name.so"
+      tmpo=$(mktemp -d)
+      make -C "$ROOT/4d_ray_tracing_amd/csrc" -s OUT="$tmpo" EXTRA="$flags" >/dev/null
+      cp "$tmpo/librt4.so" "$VDIR/$name.so"
+      rm -rf "$tmpo"
     else
       tmp=$(mktemp -d)
       git -C "$ROOT" archive "$rev" 4d_ray_tracing_amd/csrc include | tar -x -C "$tmp"

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Phase shares of the trace loop from the -DRT4_STAMPS diagnostic build (never the shipped one).
+Usage: python tools/stamps.py [scene] [spp] [bounces]   (loads 4d_ray_tracing_amd/lib/librt4_stamps.so)"""
+import importlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["RT4_LIB"] = os.path.join(ROOT, "4d_ray_tracing_amd", "lib", "librt4_stamps.so")
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+rt4 = importlib.import_module("4d_ray_tracing_amd")
+scene = sys.argv[1] if len(sys.argv) > 1 else "sphere"
+spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+bounces = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+t = rt4.Tracer(0, rt4.FLAG_SAMPLER_LUT, rt4.Scene.named(scene))
+u = rt4.make_uniforms(1920, 1080, samples=spp, reflections=bounces, seed=12345)
+frame = torch.zeros((1080, 1920, 4), device="cuda")
+cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+t.render_device(u, rt4.region(1920, 1080), frame.data_ptr(), 1920, cnt.data_ptr(), s)
+torch.cuda.synchronize()
+cnt.zero_()
+for _ in range(3):
+    t.render_device(u, rt4.region(1920, 1080), frame.data_ptr(), 1920, cnt.data_ptr(), s)
+torch.cuda.synchronize()
+c = cnt.cpu().tolist()
+total = c[6]
+names = ["refill", "find", "miss(final_light)", "resolve+material", "rand_drct", "total"]
+print(f"{scene} spp={spp} bounces={bounces} intersections={c[0]//3}")
+for i, n in enumerate(names):
+    print(f"  {n:>20s} {c[1 + i] / total * 100:6.1f}%   {c[1 + i] / max(c[0], 1):8.1f} cycles/intersection")
