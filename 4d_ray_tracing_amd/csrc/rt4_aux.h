@@ -54,6 +54,7 @@ struct SceneAux {
   float tiger_gt[RT4_MAX_TIGERS][2];   // [0]: gt(outer_cyl2.r) filters faces 1xx; [1]: gt(outer_cyl1.r) filters 2xx
   float tiger_lt[RT4_MAX_TIGERS][2];   // [0]: lt(inner_cyl2.r);                    [1]: lt(inner_cyl1.r)
   DivC sun_ang;
+  DivC sun_len;  // length(sun.drct) (fma dot + correctly rounded sqrt, as the kernel would compute it)
   PrimEntry prims[MAX_PRIMS];
 };
 

@@ -109,7 +109,8 @@ __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, 
   if (S->final_light_mode == RT4_FINAL_LIGHT_CONSTANT) return ld3(S->final_light_const);
   V3 sky = ld3(S->sky_light);
   V4 sd = ld4(S->sun.drct);
-  float deviation = acos_(dot(drct, sd) / length(drct) / length(sd));  // angle(), :45-50
+  // angle(), :45-50: (dot / length(drct)) / length(sun.drct); the second length is a scene constant
+  float deviation = acos_(div_c(dot(drct, sd) / length(drct), X->sun_len));
   float ang = S->sun.angular_size;
   if (deviation < ang) {
     float k = div_c(deviation, X->sun_ang), s = S->sun.sharpness;
@@ -133,10 +134,22 @@ __device__ __forceinline__ uint32_t rand_bits(RngState& r) {  // 23 mantissa bit
 __device__ __forceinline__ float bits_to_rand(uint32_t m) { return __uint_as_float(m | 0x3F800000u) - 1.0f; }  // :117
 __device__ __forceinline__ float rand_(RngState& r) { return bits_to_rand(rand_bits(r)); }
 
+// Index of the sampler-table entry the next diffuse bounce will read: rand() call #2 after now
+// (#1 is rand_outcome, shader.frag:488; #2 is rand_drct's w, :154). Pure function of the counter.
+__device__ __forceinline__ uint32_t next_diffuse_w_index(const RngState& r) {
+  return hash_u32(r.base ^ (r.iter + 2u * 0x79A010A9u)) & 0x007FFFFFu;
+}
+
+// w_pre: wlut[next_diffuse_w_index()] loaded at the top of the iteration (LUT path only)
 template <bool LUT>
-__device__ __forceinline__ V4 rand_drct(RngState& rng, const float* __restrict__ wlut) {  // :153-158
-  const uint32_t m = rand_bits(rng);
-  const float w = LUT ? wlut[m] : w_by_volume(bits_to_rand(m), nullptr);
+__device__ __forceinline__ V4 rand_drct(RngState& rng, const float* __restrict__ wlut, float w_pre) {  // :153-158
+  float w;
+  if (LUT) {
+    rng.iter += 0x79A010A9u;  // the w draw: its value was prefetched
+    w = w_pre;
+  } else {
+    w = w_by_volume(rand_(rng), nullptr);
+  }
   const float r = __builtin_sqrtf(1.0f - w * w);
   const float z = (rand_(rng) * 2.0f - 1.0f) * r;
   const float rr = __builtin_sqrtf(r * r - z * z);
@@ -274,6 +287,8 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     }
     if (active) {
       RT4_STAMP(t_ph);
+      float w_pre = 0.0f;  // sampler-table prefetch: in flight while find_intersection runs
+      if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];
       const typename Finder<K>::R c = Finder<K>::find(S, X, ray);  // :475
       RT4_ACC(1, t_ph);
       ++n_inter;
@@ -300,7 +315,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
           ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
         } else {  // :491 redirect(rand_drct(), norm)
           RT4_STAMP(t_ph);
-          const V4 v = rand_drct<LUT>(rng, wlut);
+          const V4 v = rand_drct<LUT>(rng, wlut, w_pre);
           RT4_ACC(4, t_ph);
           const float dv = dot(v, h.norm);
           ray.drct = dv >= 0.0f ? v : mad(h.norm, -(2.0f * dv), v);
@@ -570,6 +585,11 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     a->tiger_lt[i][1] = sqrt_lt_threshold(t.inner_cyl1.r);
   }
   if (st == RT4_OK) st = make_divc(ctx, s.sun.angular_size, &a->sun_ang, err, errlen);
+  if (st == RT4_OK) {  // length(sun.drct) exactly as the device computes it (rt4_device_math.h dot/length)
+    const float* d = s.sun.drct;
+    const float len = std::sqrt(std::fmaf(d[3], d[3], std::fmaf(d[2], d[2], std::fmaf(d[1], d[1], d[0] * d[0]))));
+    st = make_divc(ctx, len, &a->sun_len, err, errlen);
+  }
   if (st != RT4_OK) return st;
   // flat primitive table (rt4_aux.h)
   int n = 0;
