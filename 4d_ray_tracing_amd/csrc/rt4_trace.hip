@@ -37,6 +37,9 @@ namespace {
 #ifndef RT4_REFILL_MIN
 #define RT4_REFILL_MIN 8
 #endif
+#ifndef RT4_LUT_PREFETCH
+#define RT4_LUT_PREFETCH 0  // measured slower (extra gathers for every lane): profiles/r01_ab.txt
+#endif
 #ifndef RT4_WAVES_PER_SIMD
 #define RT4_WAVES_PER_SIMD 1
 #endif
@@ -134,19 +137,25 @@ __device__ __forceinline__ uint32_t rand_bits(RngState& r) {  // 23 mantissa bit
 __device__ __forceinline__ float bits_to_rand(uint32_t m) { return __uint_as_float(m | 0x3F800000u) - 1.0f; }  // :117
 __device__ __forceinline__ float rand_(RngState& r) { return bits_to_rand(rand_bits(r)); }
 
+#if RT4_LUT_PREFETCH
 // Index of the sampler-table entry the next diffuse bounce will read: rand() call #2 after now
 // (#1 is rand_outcome, shader.frag:488; #2 is rand_drct's w, :154). Pure function of the counter.
 __device__ __forceinline__ uint32_t next_diffuse_w_index(const RngState& r) {
   return hash_u32(r.base ^ (r.iter + 2u * 0x79A010A9u)) & 0x007FFFFFu;
 }
+#endif
 
 // w_pre: wlut[next_diffuse_w_index()] loaded at the top of the iteration (LUT path only)
 template <bool LUT>
 __device__ __forceinline__ V4 rand_drct(RngState& rng, const float* __restrict__ wlut, float w_pre) {  // :153-158
   float w;
   if (LUT) {
+#if RT4_LUT_PREFETCH
     rng.iter += 0x79A010A9u;  // the w draw: its value was prefetched
     w = w_pre;
+#else
+    w = wlut[rand_bits(rng)];
+#endif
   } else {
     w = w_by_volume(rand_(rng), nullptr);
   }
@@ -287,8 +296,10 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     }
     if (active) {
       RT4_STAMP(t_ph);
-      float w_pre = 0.0f;  // sampler-table prefetch: in flight while find_intersection runs
+      float w_pre = 0.0f;  // optional sampler-table prefetch: in flight while find_intersection runs
+#if RT4_LUT_PREFETCH
       if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];
+#endif
       const typename Finder<K>::R c = Finder<K>::find(S, X, ray);  // :475
       RT4_ACC(1, t_ph);
       ++n_inter;

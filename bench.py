@@ -90,6 +90,19 @@ def ops_per_unit(rt4, scene, u, width, height):
     return ops / max(n, 1), n
 
 
+def pmc_traffic(config):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of the same workload
+    (profiles/pmc_<scene>.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config['scene']}.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    keys = ("width", "height_per_gpu", "spp", "bounces", "seed", "sampler_lut")
+    if any(d.get("config", {}).get(k) != config[k] for k in keys):
+        return None, None
+    return d["derived"].get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
 def main():
     args = parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,6 +210,11 @@ def main():
                 "note": "fp32 ops (fma=2) per find_intersection+shading counted by the oracle; see DESIGN.md §5",
             },
         }
+        traffic, src = pmc_traffic(line["config"])
+        line["roofline"]["traffic"] = traffic
+        if src:
+            line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per launch)"
+            line["roofline"]["algorithmic_bytes_per_launch"] = plan.width * plan.rows_per_rank * 32
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(rt4, scene, u, plan.width, plan.rows_per_rank, args.cpu_seconds)
         print(json.dumps(line), flush=True)
