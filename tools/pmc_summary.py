@@ -55,9 +55,10 @@ def main():
     m = {}
     if "SQ_INSTS_VALU" in c and "SQ_WAVES" in c:
         m["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
-    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
-        # ACTIVE_INST_VALU is in quad-cycles; a wave64 VALU op occupies 2 SIMD-32 cycles on 64 lanes
-        m["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 4 * 32)
+    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_INSTS_VALU" in c:
+        # calibrated on gfx950 (tools/calib_util.py): a fully active wave64 VALU instruction adds ~64
+        # thread-cycles, so utilisation = THREAD_CYCLES / (INSTS * 64)
+        m["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_INSTS_VALU"] * 64)
     if "GRBM_GUI_ACTIVE" in c:
         dur = sum(durations["GRBM_GUI_ACTIVE"]) / len(durations["GRBM_GUI_ACTIVE"])
         m["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / dur  # summed over 8 XCDs (MI355X_MICROARCH.md DVFS note)
@@ -82,6 +83,18 @@ def main():
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         m["hbm_bytes_per_launch"] = m["hbm_read_bytes_corrected"] + m["hbm_write_bytes"]
     out["derived"] = m
+    for log in ("trace.log", os.path.join("trace", "..", "bench.log")):
+        lp = os.path.join(d, log)
+        if os.path.exists(lp):
+            lines = [l for l in open(lp) if l.startswith("{")]
+            if lines:
+                b = json.loads(lines[-1])
+                out["config"] = b["config"]
+                out["bench"] = {k: b[k] for k in ("value", "kernel_ms", "intersections_per_step")}
+                n = b["intersections_per_step"]
+                if "SQ_INSTS_VALU" in c:
+                    m["valu_lane_slots_per_intersection"] = c["SQ_INSTS_VALU"] * 64 / n
+                break
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
