@@ -40,6 +40,21 @@ static_assert(sizeof(PrimEntry) == 96, "PrimEntry is 6 x 16 B");
 constexpr int MAX_PRIMS = RT4_MAX_SPACES + RT4_MAX_SPHERES + RT4_MAX_CYLINDERS + 2 * RT4_MAX_UNIONS +
                           8 * RT4_MAX_HYPERCUBES + 4 * RT4_MAX_TIGERS;
 
+// Sphere cull (rt4_fast.h find_cand): for a ray outside the sphere (len_po >= r, len_po >= SMALL)
+// with dot_pord >= 0, sphere_cand misses iff sin_oap = RN(RN(len_po * sin_(acos_(c))) / r) >= 1,
+// c = RN(dot_pord / len_po). With d2 = dot(po,po) (len_po = RN(sqrt(d2))) and
+//   P = RN(d2 - RN(dot_pord^2)) > RN(fma(K, d2, r2m)),   K = 4e-6, r2m = RN(r^2 (1 + 1e-4)),
+// the exact path is guaranteed to miss: sin_(acos_(c)) is within 1.75e-7 (relative) of
+// sqrt(1 - c^2) for every float c in [0, 1) (exhaustive), the rounding of c costs at
+// most 2u c^2/(1-c^2) <= 2u d2/P relative in 1 - c^2, and P's own rounding at most 3u d2; together
+// P >= r^2 (1 + 7e-7) + 3.1e-7 d2 suffices, which the test exceeds ~13x (d2 term) / ~140x (r^2).
+// Culled spheres are exactly the ones the exact path reports as no hit, so results are unchanged.
+constexpr float SPHERE_CULL_K = 4e-6f;
+struct SphereCull {
+  float d2_out;  // smallest d2 with RN(sqrt(d2)) >= max(r, SMALL_F)
+  float r2m;     // RN(r^2 (1 + 1e-4)); +inf disables the cull (tiny or non-finite r)
+};
+
 struct SceneAux {
   // flat primitive ids: spaces, spheres, cylinders, union cylinders (2 per union), cubes (8 per
   // hypercube), tiger cylinders (inner1, outer1, inner2, outer2 per tiger)
@@ -55,6 +70,10 @@ struct SceneAux {
   float tiger_lt[RT4_MAX_TIGERS][2];   // [0]: lt(inner_cyl2.r);                    [1]: lt(inner_cyl1.r)
   DivC sun_ang;
   DivC sun_len;  // length(sun.drct) (fma dot + correctly rounded sqrt, as the kernel would compute it)
+  float sky_c_star;  // every v_cos <= this gives acos(v_cos) >= angular_size: plain sky, no acos needed
+                     // (largest float below min{c : acos(c) < angular_size}, exhaustive device search)
+  int32_t pad2_[3];
+  SphereCull sphere_cull[RT4_MAX_SPHERES];
   PrimEntry prims[MAX_PRIMS];
 };
 

@@ -11,6 +11,10 @@
 #include "rt4_aux.h"
 #include "rt4_intersect.h"
 
+#ifndef RT4_SPHERE_CULL
+#define RT4_SPHERE_CULL 1
+#endif
+
 namespace rt4 {
 
 // x / b with the verified 3-op form when allowed (uniform branch: c.fast is a scene constant).
@@ -237,33 +241,70 @@ __device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict_
   return res;
 }
 
-template <uint32_t K>
-__device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                          const Ray& ray) {
-  Cand inter = no_cand();
-  if (K & K_SPACES) {
-    const int n = S->n_spaces;
-    for (int i = 0; i < n; i++) inter = closest(space_cand(S, i, ray), inter);
+// SH = shape bits (low 8 bits, K_*) | (n_spaces+1) << 8 | (n_spheres+1) << 16 | (n_cylinders+1) << 24;
+// a zero count field means "read the count from the scene" (runtime loop).
+constexpr uint32_t sh_count(uint32_t sh, int field) { return (sh >> (8 * field)) & 0xFFu; }
+
+// for (i < count) body(i): fully unrolled when the count field C is a compile-time count
+template <uint32_t C, typename F>
+__device__ __forceinline__ void for_count(int runtime_n, F&& body) {
+  if constexpr (C != 0) {
+#pragma unroll
+    for (int i = 0; i < static_cast<int>(C) - 1; i++) body(i);
+  } else {
+    for (int i = 0; i < runtime_n; i++) body(i);
   }
+}
+
+template <uint32_t SH>
+__device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                          const PrimEntry* P, const Ray& ray) {
+  constexpr uint32_t K = SH & 0xFFu;
+  constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2), NCY = sh_count(SH, 3);
+  Cand inter = no_cand();
+  if (K & K_SPACES) for_count<NSP>(S->n_spaces, [&](int i) { inter = closest(space_cand(S, i, ray), inter); });
   if (K & K_SPHERES) {
-    const int n = S->n_spheres;
-    for (int i = 0; i < n; i++) {
+#if RT4_SPHERE_CULL
+    // Pass 1 (every sphere, ~20 VALU): the exact early-out (outside and pointing away) plus a
+    // conservative "clearly missed" test; only the remaining spheres are marked pending.
+    // Pass 2: each lane evaluates ITS pending spheres in index order, so a wave pays for
+    // max-over-lanes(pending) exact evaluations instead of n_spheres (rt4_aux.h SphereCull for the
+    // error bound that makes the cull exact).
+    uint32_t pend = 0;
+    for_count<NSH>(S->n_spheres, [&](int i) {
+      const V4 po = sub(ld4(S->spheres[i].center), ray.point);
+      const float d2 = dot(po, po);  // exactly the dot whose sqrt is len_po in sphere_cand
+      const float dp = dot(po, ray.drct);
+      const SphereCull& k = X->sphere_cull[i];
+      const bool outside = d2 >= k.d2_out;  // len_po >= max(r, SMALL)
+      const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k.r2m));
+      pend |= skip ? 0u : (1u << i);
+    });
+    while (pend) {
+      const int i = __builtin_ctz(pend);
+      pend &= pend - 1u;
+      const uint32_t id = static_cast<uint32_t>(X->base_sphere + i);
+      const PrimEntry& e = P[id];
+      const DivC dc{e.r, e.y, e.fast, 0};
+      inter = closest(sphere_cand(ld4(e.p), e.r, dc, ray, true, id), inter);
+    }
+#else
+    for_count<NSH>(S->n_spheres, [&](int i) {
       const rt4_sphere& sp = S->spheres[i];
       inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true,
                                   static_cast<uint32_t>(X->base_sphere + i)),
                       inter);
-    }
+    });
+#endif
   }
-  if (K & K_CYLINDERS) {
-    const int n = S->n_cylinders;
-    for (int i = 0; i < n; i++) {
+  if (K & K_CYLINDERS)
+    for_count<NCY>(S->n_cylinders, [&](int i) {
       const rt4_cylinder& c = S->cylinders[i];
       const V4 cp = ld4(c.point);
       inter = closest(cyl_cand(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], true,
                                static_cast<uint32_t>(X->base_cyl + i)),
                       inter);
-    }
-  }
+    });
   if (K & K_UNION) inter = closest(union_cand(S, X, 0, ray), inter);
   if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, X, 0, ray), inter);
   if (K & K_TIGER) inter = closest(tiger_cand(S, X, 0, ray), inter);
@@ -280,8 +321,9 @@ __device__ __forceinline__ V4 cyl_normal(V4 cp, V4 a1, V4 a2, float r, const Div
 
 // Normal of the winning candidate from its LDS primitive entry; Hit.mat = the flat primitive index.
 // Only the kinds the scene shape K can produce are compiled in.
-template <uint32_t K>
+template <uint32_t SH>
 __device__ __forceinline__ Hit resolve(const PrimEntry* P, const Ray& ray, const Cand& c) {
+  constexpr uint32_t K = SH & 0xFFu;
   const PrimEntry& e = P[c.id];
   const int kind = e.kind;
   Hit h;

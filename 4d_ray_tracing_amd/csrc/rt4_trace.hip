@@ -38,7 +38,10 @@ namespace {
 #define RT4_REFILL_MIN 8
 #endif
 #ifndef RT4_LUT_PREFETCH
-#define RT4_LUT_PREFETCH 0  // measured slower (extra gathers for every lane): profiles/r01_ab.txt
+#define RT4_LUT_PREFETCH 2  // 1: at loop top (measured slower), 2: at a hit (faster): profiles/r01_ab.txt
+#endif
+#ifndef RT4_SKY_THRESHOLD
+#define RT4_SKY_THRESHOLD 1
 #endif
 #ifndef RT4_WAVES_PER_SIMD
 #define RT4_WAVES_PER_SIMD 1
@@ -75,8 +78,8 @@ template <uint32_t K>
 struct Finder {
   using R = Cand;
   static __device__ __forceinline__ Cand find(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                              const Ray& ray) {
-    return find_cand<K>(S, X, ray);
+                                              const PrimEntry* P, const Ray& ray) {
+    return find_cand<K>(S, X, P, ray);
   }
   static __device__ __forceinline__ Hit resolve(const PrimEntry* P, const Ray& ray, const Cand& c) {
     return rt4::resolve<K>(P, ray, c);
@@ -93,7 +96,7 @@ template <>
 struct Finder<GENERIC> {
   using R = Hit;
   static __device__ __forceinline__ Hit find(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__,
-                                             const Ray& ray) {
+                                             const PrimEntry*, const Ray& ray) {
     return find_intersection_generic(S, ray);
   }
   static __device__ __forceinline__ Hit resolve(const PrimEntry*, const Ray&, const Hit& h) { return h; }
@@ -113,8 +116,12 @@ __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, 
   V3 sky = ld3(S->sky_light);
   V4 sd = ld4(S->sun.drct);
   // angle(), :45-50: (dot / length(drct)) / length(sun.drct); the second length is a scene constant
-  float deviation = acos_(div_c(dot(drct, sd) / length(drct), X->sun_len));
+  const float vcos = div_c(dot(drct, sd) / length(drct), X->sun_len);
   float ang = S->sun.angular_size;
+#if RT4_SKY_THRESHOLD
+  if (!(vcos > X->sky_c_star)) return sky;  // acos(vcos) >= ang (or NaN): the sky branch, exactly
+#endif
+  float deviation = acos_(vcos);
   if (deviation < ang) {
     float k = div_c(deviation, X->sun_ang), s = S->sun.sharpness;
     k = (s * s * k / (1.0f - s * k) + 1.0f) * (1.0f - k);
@@ -297,10 +304,10 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     if (active) {
       RT4_STAMP(t_ph);
       float w_pre = 0.0f;  // optional sampler-table prefetch: in flight while find_intersection runs
-#if RT4_LUT_PREFETCH
+#if RT4_LUT_PREFETCH == 1
       if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];
 #endif
-      const typename Finder<K>::R c = Finder<K>::find(S, X, ray);  // :475
+      const typename Finder<K>::R c = Finder<K>::find(S, X, P, ray);  // :475
       RT4_ACC(1, t_ph);
       ++n_inter;
       bool end;
@@ -311,6 +318,9 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
         end = true;
       } else {
+#if RT4_LUT_PREFETCH == 2
+        if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];  // in flight during resolve + shading
+#endif
         RT4_STAMP(t_ph);
         const Hit h = Finder<K>::resolve(P, ray, c);
         float glow, refl;
@@ -382,6 +392,21 @@ __global__ void rt4_verify_div_kernel(float b, float y, unsigned* __restrict__ m
   if (bad) atomicAdd(mismatches, bad);
 }
 
+// min over all float patterns c with acos_(c) < ang, as an order-preserving key (0xFFFFFFFF: none)
+__device__ __forceinline__ uint32_t order_key(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__global__ void rt4_sky_threshold_kernel(float ang, uint32_t* __restrict__ best) {
+  uint32_t mine = 0xFFFFFFFFu;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+    const float c = __uint_as_float(static_cast<uint32_t>(i));
+    if (acos_(c) < ang) mine = min(mine, order_key(c));
+  }
+  if (mine != 0xFFFFFFFFu) atomicMin(best, mine);
+}
+
 __global__ void rt4_eval_kernel(int fn, const float* __restrict__ in, float* __restrict__ out, int32_t* __restrict__ aux,
                                 int64_t n) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -411,7 +436,7 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const Scen
   if (t >= n) return;
   const float* r = rays + 8 * t;
   const Ray ray{ld4(r), ld4(r + 4)};
-  const typename Finder<K>::R c = Finder<K>::find(S, X, ray);
+  const typename Finder<K>::R c = Finder<K>::find(S, X, X->prims, ray);
   Hit h = c.hit ? Finder<K>::resolve(X->prims, ray, c) : no_hit();
   h.dist = c.dist;
   float* o = out + 8 * t;
@@ -442,6 +467,8 @@ struct Variant {
 };
 
 #define RT4_VARIANT(K) {K, {rt4_trace_kernel<K, false>, rt4_trace_kernel<K, true>}, rt4_find_kernel<K>}
+// shape | (n_spaces+1) << 8 | (n_spheres+1) << 16 | (n_cylinders+1) << 24 (rt4_fast.h sh_count)
+#define SH(K, nsp, nsh, ncy) ((K) | (uint32_t(nsp) << 8) | (uint32_t(nsh) << 16) | (uint32_t(ncy) << 24))
 const Variant kVariants[] = {
     RT4_VARIANT(GENERIC),
     RT4_VARIANT(K_SPACES),
@@ -450,8 +477,17 @@ const Variant kVariants[] = {
     RT4_VARIANT(K_SPACES | K_HYPERCUBE),
     RT4_VARIANT(K_SPACES | K_TIGER),
     RT4_VARIANT(K_SPACES | K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE | K_TIGER),
+    // exact object counts of the reference scenes and the authored ones: fully unrolled
+    RT4_VARIANT(SH(K_SPACES | K_SPHERES, 2, 3, 0)),      // sphere
+    RT4_VARIANT(SH(K_SPACES | K_SPHERES, 9, 3, 0)),      // room
+    RT4_VARIANT(SH(K_SPACES | K_TIGER, 2, 0, 0)),        // tiger
+    RT4_VARIANT(SH(K_SPACES | K_TIGER, 4, 0, 0)),        // tiger_two_mirrors
+    RT4_VARIANT(SH(K_SPACES | K_UNION, 2, 0, 0)),        // cylinder4d
+    RT4_VARIANT(SH(K_SPACES | K_HYPERCUBE, 2, 0, 0)),    // hypercube
+    RT4_VARIANT(SH(K_SPACES | K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE | K_TIGER, 3, 4, 2)),  // all_primitives
 };
 #undef RT4_VARIANT
+#undef SH
 
 bool same4(const float* a, const float* b) { return std::memcmp(a, b, 4 * sizeof(float)) == 0; }
 
@@ -485,6 +521,11 @@ uint32_t scene_shape(const rt4_scene_desc& s) {
     if (gr.count != n) return GENERIC;
     k |= bit[gr.kind];
   }
+  const uint32_t counted = k | (static_cast<uint32_t>(s.n_spaces + 1) << 8) |
+                           (static_cast<uint32_t>(s.n_spheres + 1) << 16) |
+                           (static_cast<uint32_t>(s.n_cylinders + 1) << 24);
+  for (const Variant& v : kVariants)  // exact counts first (unrolled), then the runtime-count kernel
+    if (v.shape == counted) return counted;
   for (const Variant& v : kVariants)
     if (v.shape == k) return k;
   return GENERIC;
@@ -580,6 +621,12 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
   std::memset(a, 0, sizeof *a);
   int st = RT4_OK;
   for (int i = 0; i < s.n_spheres && st == RT4_OK; i++) st = make_divc(ctx, s.spheres[i].r, &a->sphere_r[i], err, errlen);
+  for (int i = 0; i < s.n_spheres; i++) {  // rt4_aux.h SphereCull
+    const float r = s.spheres[i].r;
+    a->sphere_cull[i].d2_out = sqrt_lt_threshold(std::max(r, 0.0003f));  // SMALL_F, shader.frag:24
+    const bool ok = r >= 1e-15f && r <= 1e15f;  // r <= 0: sin_oap < 1 always, never cull
+    a->sphere_cull[i].r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
+  }
   for (int i = 0; i < s.n_cylinders && st == RT4_OK; i++) st = make_divc(ctx, s.cylinders[i].r, &a->cyl_r[i], err, errlen);
   for (int i = 0; i < s.n_unions && st == RT4_OK; i++) {
     st = make_divc(ctx, s.unions[i].cylinder1.r, &a->union_r[i][0], err, errlen);
@@ -596,6 +643,24 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     a->tiger_lt[i][1] = sqrt_lt_threshold(t.inner_cyl1.r);
   }
   if (st == RT4_OK) st = make_divc(ctx, s.sun.angular_size, &a->sun_ang, err, errlen);
+  if (st == RT4_OK && s.final_light_mode == RT4_FINAL_LIGHT_SUN_SKY) {  // sky threshold (rt4_aux.h)
+    const uint32_t init = 0xFFFFFFFFu;
+    HIP_TRY(hipMemcpy(ctx->d_scratch, &init, sizeof init, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(rt4_sky_threshold_kernel, dim3(65536), dim3(256), 0, 0, s.sun.angular_size, ctx->d_scratch);
+    HIP_TRY(hipGetLastError());
+    uint32_t best = 0;
+    HIP_TRY(hipMemcpy(&best, ctx->d_scratch, sizeof best, hipMemcpyDeviceToHost));
+    if (best == 0xFFFFFFFFu) {
+      a->sky_c_star = INFINITY;  // acos never below the angular size: always sky
+    } else {
+      const uint32_t bits = (best & 0x80000000u) ? (best & 0x7FFFFFFFu) : ~best;
+      float m;
+      std::memcpy(&m, &bits, 4);
+      a->sky_c_star = std::nextafter(m, -INFINITY);
+    }
+  } else {
+    a->sky_c_star = -INFINITY;
+  }
   if (st == RT4_OK) {  // length(sun.drct) exactly as the device computes it (rt4_device_math.h dot/length)
     const float* d = s.sun.drct;
     const float len = std::sqrt(std::fmaf(d[3], d[3], std::fmaf(d[2], d[2], std::fmaf(d[1], d[1], d[0] * d[0]))));

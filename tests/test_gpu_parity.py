@@ -92,6 +92,50 @@ def test_find_intersection_bitwise(rt4, oracle, name, generic):
         t.close()
 
 
+def grazing_rays(centers, radii, n_per, seed):
+    """Rays passing sphere i at perpendicular distance r_i (1 + e), |e| from 1e-8 to 1e-1 and both
+    signs, from outside (2r..60r away): the boundary of the sphere cull (rt4_aux.h SphereCull)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for c, r in zip(centers, radii):
+        c = np.asarray(c, np.float64)
+        u = rng.normal(size=(n_per, 4))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        v = rng.normal(size=(n_per, 4))
+        v -= (v * u).sum(1, keepdims=True) * u
+        v /= np.linalg.norm(v, axis=1, keepdims=True)
+        L = r * np.exp(rng.uniform(np.log(2.0), np.log(60.0), n_per))[:, None]
+        e = np.where(rng.random(n_per) < 0.5, -1.0, 1.0) * 10.0 ** rng.uniform(-8, -1, n_per)
+        e[: n_per // 16] = 0.0
+        sa = np.clip(r * (1.0 + e)[:, None] / L, 0.0, 1.0)
+        d = -u * np.sqrt(1.0 - sa * sa) + v * sa
+        out.append(np.concatenate([c + L * u, d], axis=1))
+    return np.concatenate(out).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["sphere", "room", "all_primitives"])
+def test_find_intersection_grazing_spheres(rt4, oracle, name):
+    scene = rt4.Scene.named(name)
+    d = scene.desc
+    centers = [list(d.spheres[i].center) for i in range(d.n_spheres)]
+    radii = [d.spheres[i].r for i in range(d.n_spheres)]
+    rays = grazing_rays(centers, radii, 40000, 77)
+    c, cc = oracle.find_intersection(scene.desc, rays)
+    t = rt4.Tracer(device=0, scene=scene)
+    try:
+        g, gc = t.debug_find_intersection(rays)
+    finally:
+        t.close()
+    assert_bits(g, c, f"{name} grazing find_intersection")
+    assert_bits(gc, cc, f"{name} grazing material color")
+    # many of the hits are the spheres themselves (normal unlike every space's), near the tangent
+    sn = np.array([list(d.spaces[i].norm) for i in range(d.n_spaces)], np.float32)
+    on_space = np.zeros(len(c), bool)
+    for n in sn:
+        on_space |= np.all(np.abs(np.abs(c[:, 2:6]) - np.abs(n)) < 1e-6, axis=1)
+    assert ((c[:, 0] > 0) & ~on_space).mean() > 0.05
+
+
 # -------------------------------------------------------------------------------------- images
 def render_both(rt4, oracle, scene, u, reg, flags=0, old=None):
     t = rt4.Tracer(device=0, flags=flags, scene=scene)
