@@ -467,8 +467,10 @@ struct Variant {
 };
 
 #define RT4_VARIANT(K) {K, {rt4_trace_kernel<K, false>, rt4_trace_kernel<K, true>}, rt4_find_kernel<K>}
-// shape | (n_spaces+1) << 8 | (n_spheres+1) << 16 | (n_cylinders+1) << 24 (rt4_fast.h sh_count)
-#define SH(K, nsp, nsh, ncy) ((K) | (uint32_t(nsp) << 8) | (uint32_t(nsh) << 16) | (uint32_t(ncy) << 24))
+// shape | (n_spaces+1) << 8 | (n_spheres+1) << 16 | (n_cylinders+1) << 24 (rt4_fast.h sh_count),
+// from the scene's object counts (the same encoding scene_shape() computes)
+#define SH(K, nsp, nsh, ncy) \
+  ((K) | (uint32_t((nsp) + 1) << 8) | (uint32_t((nsh) + 1) << 16) | (uint32_t((ncy) + 1) << 24))
 const Variant kVariants[] = {
     RT4_VARIANT(GENERIC),
     RT4_VARIANT(K_SPACES),
@@ -478,13 +480,13 @@ const Variant kVariants[] = {
     RT4_VARIANT(K_SPACES | K_TIGER),
     RT4_VARIANT(K_SPACES | K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE | K_TIGER),
     // exact object counts of the reference scenes and the authored ones: fully unrolled
-    RT4_VARIANT(SH(K_SPACES | K_SPHERES, 2, 3, 0)),      // sphere
-    RT4_VARIANT(SH(K_SPACES | K_SPHERES, 9, 3, 0)),      // room
-    RT4_VARIANT(SH(K_SPACES | K_TIGER, 2, 0, 0)),        // tiger
-    RT4_VARIANT(SH(K_SPACES | K_TIGER, 4, 0, 0)),        // tiger_two_mirrors
-    RT4_VARIANT(SH(K_SPACES | K_UNION, 2, 0, 0)),        // cylinder4d
-    RT4_VARIANT(SH(K_SPACES | K_HYPERCUBE, 2, 0, 0)),    // hypercube
-    RT4_VARIANT(SH(K_SPACES | K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE | K_TIGER, 3, 4, 2)),  // all_primitives
+    RT4_VARIANT(SH(K_SPACES | K_SPHERES, 1, 2, 0)),      // sphere
+    RT4_VARIANT(SH(K_SPACES | K_SPHERES, 8, 2, 0)),      // room
+    RT4_VARIANT(SH(K_SPACES | K_TIGER, 1, 0, 0)),        // tiger
+    RT4_VARIANT(SH(K_SPACES | K_TIGER, 3, 0, 0)),        // tiger_two_mirrors
+    RT4_VARIANT(SH(K_SPACES | K_UNION, 1, 0, 0)),        // cylinder4d
+    RT4_VARIANT(SH(K_SPACES | K_HYPERCUBE, 1, 0, 0)),    // hypercube
+    RT4_VARIANT(SH(K_SPACES | K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE | K_TIGER, 2, 3, 1)),  // all_primitives
 };
 #undef RT4_VARIANT
 #undef SH
@@ -524,8 +526,10 @@ uint32_t scene_shape(const rt4_scene_desc& s) {
   const uint32_t counted = k | (static_cast<uint32_t>(s.n_spaces + 1) << 8) |
                            (static_cast<uint32_t>(s.n_spheres + 1) << 16) |
                            (static_cast<uint32_t>(s.n_cylinders + 1) << 24);
+#ifndef RT4_NO_EXACT_COUNTS  // A/B knob: -DRT4_NO_EXACT_COUNTS runs every scene on its runtime-count kernel
   for (const Variant& v : kVariants)  // exact counts first (unrolled), then the runtime-count kernel
     if (v.shape == counted) return counted;
+#endif
   for (const Variant& v : kVariants)
     if (v.shape == k) return k;
   return GENERIC;
@@ -777,6 +781,8 @@ int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* e
   ctx->has_scene = true;
   return RT4_OK;
 }
+
+uint32_t rt4_context_kernel_shape(const rt4_context* ctx) { return ctx && ctx->has_scene ? ctx->shape : 0u; }
 
 int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
                       int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err, size_t errlen) {

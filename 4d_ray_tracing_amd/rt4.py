@@ -159,6 +159,7 @@ def _load():
         "rt4_render_host": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int64, POINTER(c_uint64)] + E, c_int),
         "rt4_debug_eval": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64] + E, c_int),
         "rt4_debug_find_intersection": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int64] + E, c_int),
+        "rt4_context_kernel_shape": ([c_void_p], c_uint32),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)  # AttributeError if the library lacks a declared export
@@ -174,7 +175,7 @@ EXPORTED = (
     "rt4_properties_get_float rt4_properties_get_bool rt4_orientation_update rt4_section_basis "
     "rt4_uniforms_from_properties rt4_window_cells rt4_scene_load_frag rt4_scene_parse_frag rt4_scene_validate "
     "rt4_scene_builtin rt4_context_create rt4_context_set_scene rt4_context_destroy rt4_render_device rt4_render_host "
-    "rt4_debug_eval rt4_debug_find_intersection"
+    "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -392,6 +393,11 @@ class Tracer:
         _check(lib.rt4_render_host(self._h, byref(u), byref(reg), c_void_p(frame.ctypes.data), stride, byref(n), err,
                                    len(err)), err)
         return n.value
+
+    @property
+    def kernel_shape(self) -> int:
+        """Shape code of the trace kernel the scene runs on (rt4.h rt4_context_kernel_shape)."""
+        return lib.rt4_context_kernel_shape(self._h)
 
     def debug_eval(self, fn: int, x):
         import numpy as np

@@ -290,6 +290,13 @@ int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_
 int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out, float* out_color, int64_t n,
                                 char* err, size_t errlen);
 
+/* Trace kernel selected for the context's scene: 0xFFFFFFFF = the generic find_intersection
+ * (any group list); otherwise the K_* group bits (low byte: 1 spaces, 2 spheres, 4 cylinders,
+ * 8 union, 16 hypercube, 32 tiger), plus (n_spaces+1) << 8 | (n_spheres+1) << 16 |
+ * (n_cylinders+1) << 24 when a kernel compiled for the scene's exact object counts exists.
+ * 0 if the context has no scene. */
+uint32_t rt4_context_kernel_shape(const rt4_context* ctx);
+
 #ifdef __cplusplus
 }
 #endif

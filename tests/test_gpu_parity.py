@@ -66,6 +66,30 @@ def test_w_by_volume_exhaustive(tracer, rt4, oracle):
     assert gi.max() < 64  # the loop cap is never reached
 
 
+# --------------------------------------------------------------------------- kernel selection
+EXACT_COUNTS = {  # scene -> (group bits, n_spaces, n_spheres, n_cylinders): rt4_trace.hip kVariants
+    "sphere": (0x03, 1, 2, 0), "room": (0x03, 8, 2, 0), "tiger": (0x21, 1, 0, 0),
+    "tiger_two_mirrors": (0x21, 3, 0, 0), "cylinder4d": (0x09, 1, 0, 0), "hypercube": (0x11, 1, 0, 0),
+    "all_primitives": (0x3F, 2, 3, 1),
+}
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_scene_runs_exact_count_kernel(rt4, name):
+    """Every reference and authored scene gets the kernel compiled for its exact object counts."""
+    k, nsp, nsh, ncy = EXACT_COUNTS[name]
+    t = rt4.Tracer(device=0, scene=rt4.Scene.named(name))
+    try:
+        assert t.kernel_shape == k | (nsp + 1) << 8 | (nsh + 1) << 16 | (ncy + 1) << 24
+    finally:
+        t.close()
+    t = rt4.Tracer(device=0, scene=rt4.Scene.named(name), flags=rt4.FLAG_GENERIC_KERNEL)
+    try:
+        assert t.kernel_shape == 0xFFFFFFFF
+    finally:
+        t.close()
+
+
 # ------------------------------------------------------------------------------- intersections
 def random_rays(n, seed):
     rng = np.random.default_rng(seed)
