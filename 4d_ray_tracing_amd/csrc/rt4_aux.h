@@ -72,7 +72,10 @@ struct SceneAux {
   DivC sun_len;  // length(sun.drct) (fma dot + correctly rounded sqrt, as the kernel would compute it)
   float sky_c_star;  // every v_cos <= this gives acos(v_cos) >= angular_size: plain sky, no acos needed
                      // (largest float below min{c : acos(c) < angular_size}, exhaustive device search)
-  int32_t pad2_[3];
+  float sky_pre_k;   // conservative sky pre-test (trace final_light): a <= 0 || a*a < l2 * sky_pre_k with
+                     // a = dot(drct, sun.drct), l2 = dot(drct, drct) in [2^-40, 2^40] implies
+                     // v_cos <= sky_c_star. sky_pre_k = RN(c*^2 len(sun)^2 (1 - 1e-5)); 0 disables.
+  int32_t pad2_[2];
   SphereCull sphere_cull[RT4_MAX_SPHERES];
   PrimEntry prims[MAX_PRIMS];
 };

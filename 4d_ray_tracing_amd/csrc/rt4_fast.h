@@ -245,6 +245,16 @@ __device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict_
 // a zero count field means "read the count from the scene" (runtime loop).
 constexpr uint32_t sh_count(uint32_t sh, int field) { return (sh >> (8 * field)) & 0xFFu; }
 
+// Primitive-table entries of a shape (rt4_aux.h SceneAux::prims): exact for exact-count shapes,
+// MAX_PRIMS when a count is read at run time. Sizes the kernel's LDS copy of the table.
+constexpr int n_prims_of(uint32_t sh) {
+  const uint32_t k = sh & 0xFFu;
+  if (sh_count(sh, 1) == 0 || sh_count(sh, 2) == 0 || sh_count(sh, 3) == 0) return MAX_PRIMS;
+  const int n = static_cast<int>(sh_count(sh, 1) + sh_count(sh, 2) + sh_count(sh, 3)) - 3 + ((k & K_UNION) ? 2 : 0) +
+                ((k & K_HYPERCUBE) ? 8 : 0) + ((k & K_TIGER) ? 4 : 0);
+  return n > 0 ? n : 1;
+}
+
 // for (i < count) body(i): fully unrolled when the count field C is a compile-time count
 template <uint32_t C, typename F>
 __device__ __forceinline__ void for_count(int runtime_n, F&& body) {

@@ -335,7 +335,9 @@ int rt4_check_render_args(const rt4_uniforms* u, const rt4_region* r, long long 
   if (r->band_rows < 0 || (r->band_rows > 0 && r->band_step < r->band_rows))
     return rt4_set_err(err, errlen, "bad band layout (band_rows %d, band_step %d)", r->band_rows, r->band_step),
            RT4_ERR_ARG;
-  if (r->w > 65535 * 16 || r->h > 65535 * 16) return rt4_set_err(err, errlen, "region too large"), RT4_ERR_ARG;
+  // the kernel packs a region-local pixel as j | i << 16 (rt4_trace.hip, RT4_COLD_LDS)
+  if (r->w > 65535 || r->h > 32767)
+    return rt4_set_err(err, errlen, "region too large (%d x %d; at most 65535 x 32767)", r->w, r->h), RT4_ERR_ARG;
   if (u->samples < 0 || u->reflections_amount < 0)
     return rt4_set_err(err, errlen, "samples/reflections_amount must be >= 0"), RT4_ERR_ARG;
   if (!(u->resolution[0] > 0.0f) || !(u->resolution[1] > 0.0f))

@@ -38,10 +38,29 @@ namespace {
 #define RT4_REFILL_MIN 8
 #endif
 #ifndef RT4_LUT_PREFETCH
-#define RT4_LUT_PREFETCH 2  // 1: at loop top (measured slower), 2: at a hit (faster): profiles/r01_ab.txt
+// When the sampler-table entry of a possible diffuse bounce is fetched: 2 = at a hit, in flight
+// during resolve + shading; 0 = in rand_drct. Measured alternatives, all slower (profiles/r01_ab.txt):
+// at the top of every iteration; at the top for lanes that can hit; at a hit by LDS-DMA.
+#define RT4_LUT_PREFETCH 2
 #endif
 #ifndef RT4_SKY_THRESHOLD
 #define RT4_SKY_THRESHOLD 1
+#endif
+#ifndef RT4_LUT2
+#define RT4_LUT2 0  // 1: the sampler table holds {w, sqrt(1 - w*w)} (rand_drct's first sqrt tabulated too)
+#endif
+#if RT4_LUT2
+using WEntry = float2;
+__device__ __forceinline__ float went_w(WEntry e) { return e.x; }
+#else
+using WEntry = float;
+__device__ __forceinline__ float went_w(WEntry e) { return e; }
+#endif
+#ifndef RT4_COLD_LDS
+#define RT4_COLD_LDS 1  // per-lane state touched once per sample (d0, light sum, pixel) lives in LDS
+#endif
+#ifndef RT4_SKY_PRETEST
+#define RT4_SKY_PRETEST 1
 #endif
 #ifndef RT4_WAVES_PER_SIMD
 #define RT4_WAVES_PER_SIMD 1
@@ -115,8 +134,13 @@ __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, 
   if (S->final_light_mode == RT4_FINAL_LIGHT_CONSTANT) return ld3(S->final_light_const);
   V3 sky = ld3(S->sky_light);
   V4 sd = ld4(S->sun.drct);
+  const float a_ds = dot(drct, sd), l2 = dot(drct, drct);
+#if RT4_SKY_PRETEST
+  // clearly away from the sun: the exact v_cos below would be <= sky_c_star (rt4_aux.h sky_pre_k)
+  if (l2 >= 0x1p-40f && l2 <= 0x1p40f && (a_ds <= 0.0f || a_ds * a_ds < l2 * X->sky_pre_k)) return sky;
+#endif
   // angle(), :45-50: (dot / length(drct)) / length(sun.drct); the second length is a scene constant
-  const float vcos = div_c(dot(drct, sd) / length(drct), X->sun_len);
+  const float vcos = div_c(a_ds / __builtin_sqrtf(l2), X->sun_len);
   float ang = S->sun.angular_size;
 #if RT4_SKY_THRESHOLD
   if (!(vcos > X->sky_c_star)) return sky;  // acos(vcos) >= ang (or NaN): the sky branch, exactly
@@ -154,19 +178,25 @@ __device__ __forceinline__ uint32_t next_diffuse_w_index(const RngState& r) {
 
 // w_pre: wlut[next_diffuse_w_index()] loaded at the top of the iteration (LUT path only)
 template <bool LUT>
-__device__ __forceinline__ V4 rand_drct(RngState& rng, const float* __restrict__ wlut, float w_pre) {  // :153-158
-  float w;
+__device__ __forceinline__ V4 rand_drct(RngState& rng, const WEntry* __restrict__ wlut, WEntry w_pre) {  // :153-158
+  float w, r;
   if (LUT) {
 #if RT4_LUT_PREFETCH
     rng.iter += 0x79A010A9u;  // the w draw: its value was prefetched
-    w = w_pre;
+    const WEntry e = w_pre;
 #else
-    w = wlut[rand_bits(rng)];
+    const WEntry e = wlut[rand_bits(rng)];
+#endif
+    w = went_w(e);
+#if RT4_LUT2
+    r = e.y;  // = sqrt(1 - w*w) with the same ops, tabulated (rt4_build_wlut_kernel)
+#else
+    r = __builtin_sqrtf(1.0f - w * w);
 #endif
   } else {
     w = w_by_volume(rand_(rng), nullptr);
+    r = __builtin_sqrtf(1.0f - w * w);
   }
-  const float r = __builtin_sqrtf(1.0f - w * w);
   const float z = (rand_(rng) * 2.0f - 1.0f) * r;
   const float rr = __builtin_sqrtf(r * r - z * z);
   const float fi = rand_(rng) * 2.0f * PI_F;
@@ -204,7 +234,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         float4* __restrict__ frame,
                                                         unsigned long long* __restrict__ counter,
-                                                        const float* __restrict__ wlut, unsigned* __restrict__ queue) {
+                                                        const WEntry* __restrict__ wlut, unsigned* __restrict__ queue) {
   const unsigned lane = threadIdx.x & 63u;
   const int W = a.reg.w, H = a.reg.h;
   const unsigned tiles_x = (static_cast<unsigned>(W) + 7u) >> 3;
@@ -214,7 +244,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   const int R = a.u.reflections_amount, NS = a.u.samples;
   const uint32_t useed = static_cast<uint32_t>(a.u.seed);
   // the primitive table (normals + materials of hits) is read per lane: stage it in LDS once
-  __shared__ float4 lds_prims[K == GENERIC ? 1 : MAX_PRIMS * 6];
+  __shared__ float4 lds_prims[K == GENERIC ? 1 : n_prims_of(K) * 6];
   if constexpr (K != GENERIC) {
     const float4* src = reinterpret_cast<const float4*>(X->prims);
     const int n4 = X->n_prims * 6;
@@ -226,11 +256,20 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   unsigned b_next = 0, b_end = 0;  // wave-uniform: unclaimed part of the current batch
   bool exhausted = false;
   bool active = false, pending = false;
-  int pj = 0, pi = 0;
   RngState rng{0u, 0u};
+  Ray ray{V4{0.0f, 0.0f, 0.0f, 0.0f}, V4{0.0f, 0.0f, 0.0f, 0.0f}};
+  V3 acc{0.0f, 0.0f, 0.0f}, T{1.0f, 1.0f, 1.0f};
+#if RT4_COLD_LDS
+  // Cold per-lane state in LDS, one float4 column per lane (ds_read/write_b128, conflict-free):
+  // [0] the pixel's primary direction d0, [256] {light sum, pixel j | i << 16}. Touched once per
+  // sample, so the VGPRs go to occupancy instead.
+  __shared__ float4 lds_cold[2 * 256];
+  float4* const cold = lds_cold + threadIdx.x;
+#else
+  int pj = 0, pi = 0;
   V4 d0{0.0f, 0.0f, 0.0f, 0.0f};
-  Ray ray{d0, d0};
-  V3 acc{0.0f, 0.0f, 0.0f}, T{1.0f, 1.0f, 1.0f}, light{0.0f, 0.0f, 0.0f};
+  V3 light{0.0f, 0.0f, 0.0f};
+#endif
   int s = 0, b = 0;
   uint32_t n_inter = 0;
 
@@ -238,13 +277,22 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;
   RT4_STAMP(t_loop0);
 #endif
+#if RT4_COLD_LDS
+  auto flush_pixel = [&]() {
+    const float4 lp = cold[256];
+    const int pk = __float_as_int(lp.w);
+    write_pixel(a, frame, pk & 0xFFFF, pk >> 16, V3{lp.x, lp.y, lp.z});
+  };
+#else
+  auto flush_pixel = [&]() { write_pixel(a, frame, pj, pi, light); };
+#endif
   while (true) {
     RT4_STAMP(t_ph);
     if (!exhausted) {
       const unsigned long long idle = __ballot(!active);
       if (static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN) {
         if (pending) {
-          write_pixel(a, frame, pj, pi, light);
+          flush_pixel();
           pending = false;
         }
         const unsigned rank =
@@ -270,8 +318,6 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
             const int jj = static_cast<int>((tile % tiles_x) * 8u + (l & 7u));
             const int ii = static_cast<int>((tile / tiles_x) * 8u + (l >> 3));
             if (jj < W && ii < H) {
-              pj = jj;
-              pi = ii;
               // main(): scr_coord = gl_FragCoord.xy / resolution (shader.frag:515-516)
               const float sx = (static_cast<float>(a.reg.x0 + jj) + 0.5f) / a.u.resolution[0];
               const float sy = (static_cast<float>(region_row(a.reg, ii)) + 0.5f) / a.u.resolution[1];
@@ -279,12 +325,20 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
               // ray_drct(), shader.frag:501-505
               const float mx = (sx - 0.5f) * a.u.mtr_sizes[0];
               const float my = (0.5f - sy) * a.u.mtr_sizes[1];
-              d0 = mad(ld4(a.u.right_drct), mx, mad(ld4(a.u.top_drct), my, ld4(a.u.vec_to_mtr)));
-              d0 = divs(d0, length(d0));
-              ray = Ray{focus, d0};
+              V4 dd = mad(ld4(a.u.right_drct), mx, mad(ld4(a.u.top_drct), my, ld4(a.u.vec_to_mtr)));
+              dd = divs(dd, length(dd));
+              ray = Ray{focus, dd};
               acc = V3{0.0f, 0.0f, 0.0f};
               T = V3{1.0f, 1.0f, 1.0f};
+#if RT4_COLD_LDS
+              cold[0] = make_float4(dd.x, dd.y, dd.z, dd.w);
+              cold[256] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(jj | (ii << 16)));
+#else
+              d0 = dd;
+              pj = jj;
+              pi = ii;
               light = V3{0.0f, 0.0f, 0.0f};
+#endif
               s = 0;
               b = 0;
               active = NS > 0;
@@ -303,10 +357,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     }
     if (active) {
       RT4_STAMP(t_ph);
-      float w_pre = 0.0f;  // optional sampler-table prefetch: in flight while find_intersection runs
-#if RT4_LUT_PREFETCH == 1
-      if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];
-#endif
+      WEntry w_pre{};  // sampler-table entry for this iteration's diffuse bounce (LUT path)
       const typename Finder<K>::R c = Finder<K>::find(S, X, P, ray);  // :475
       RT4_ACC(1, t_ph);
       ++n_inter;
@@ -319,7 +370,11 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         end = true;
       } else {
 #if RT4_LUT_PREFETCH == 2
+#ifdef RT4_ABL_NOLUT  // ablation only (wrong images): the index arithmetic without the table gather
+        if (LUT) w_pre = WEntry{static_cast<float>(next_diffuse_w_index(rng)) * 2.3841858e-7f - 1.0f};
+#else
         if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];  // in flight during resolve + shading
+#endif
 #endif
         RT4_STAMP(t_ph);
         const Hit h = Finder<K>::resolve(P, ray, c);
@@ -345,10 +400,17 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         end = b > R;
       }
       if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
+#if RT4_COLD_LDS
+        const float4 lp = cold[256];
+        cold[256] = make_float4(lp.x + acc.x, lp.y + acc.y, lp.z + acc.z, lp.w);
+        const float4 c0 = cold[0];
+        ray = Ray{focus, V4{c0.x, c0.y, c0.z, c0.w}};
+#else
         light = V3{light.x + acc.x, light.y + acc.y, light.z + acc.z};
+        ray = Ray{focus, d0};
+#endif
         ++s;
         b = 0;
-        ray = Ray{focus, d0};
         acc = V3{0.0f, 0.0f, 0.0f};
         T = V3{1.0f, 1.0f, 1.0f};
         if (s >= NS) {
@@ -358,7 +420,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
       }
     }
   }
-  if (pending) write_pixel(a, frame, pj, pi, light);
+  if (pending) flush_pixel();
 #ifdef RT4_STAMPS
   RT4_ACC(5, t_loop0);
   if (counter && lane == 0)
@@ -372,9 +434,15 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   }
 }
 
-__global__ void rt4_build_wlut_kernel(float* __restrict__ lut) {
+__global__ void rt4_build_wlut_kernel(WEntry* __restrict__ lut) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < (1u << 23)) lut[m] = w_by_volume(__uint_as_float(m | 0x3F800000u) - 1.0f, nullptr);
+  if (m >= (1u << 23)) return;
+  const float w = w_by_volume(__uint_as_float(m | 0x3F800000u) - 1.0f, nullptr);
+#if RT4_LUT2
+  lut[m] = make_float2(w, __builtin_sqrtf(1.0f - w * w));
+#else
+  lut[m] = w;
+#endif
 }
 
 // Exhaustive check of div_c against the IEEE quotient for every 32-bit numerator pattern.
@@ -457,7 +525,7 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const Scen
 
 // ---------------------------------------------------------------- kernel table
 typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, float4*, unsigned long long*,
-                        const float*, unsigned*);
+                        const WEntry*, unsigned*);
 typedef void (*FindFn)(const rt4_scene_desc*, const SceneAux*, const float*, float*, float*, int64_t);
 
 struct Variant {
@@ -553,7 +621,7 @@ struct rt4_context {
   std::map<uint32_t, bool> div_ok;   // verified divisors (by bit pattern)
   bool has_scene = false;
   uint32_t shape = GENERIC;
-  float* d_wlut = nullptr;
+  WEntry* d_wlut = nullptr;
   unsigned* d_queue = nullptr;  // QUEUE_SLOTS words
   unsigned launch_seq = 0;
   int n_cu = 0;
@@ -669,6 +737,16 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     const float* d = s.sun.drct;
     const float len = std::sqrt(std::fmaf(d[3], d[3], std::fmaf(d[2], d[2], std::fmaf(d[1], d[1], d[0] * d[0]))));
     st = make_divc(ctx, len, &a->sun_len, err, errlen);
+    // Sky pre-test constant (rt4_aux.h sky_pre_k). With a*a < l2*K computed in fp32 (3 roundings) the
+    // exact ratio a / (sqrt(l2) len) is below c* (1 - 4.9e-6); the kernel's v_cos (3 more roundings)
+    // stays below c* (1 - 4.6e-6) <= c*, i.e. the sky branch. Needs c* > 0 and K well inside the
+    // normal range so that the two products cannot underflow or overflow for l2 in [2^-40, 2^40].
+    a->sky_pre_k = 0.0f;
+    const double c = a->sky_c_star;
+    if (s.final_light_mode == RT4_FINAL_LIGHT_SUN_SKY && std::isfinite(c) && c > 0.0 && std::isfinite(len) && len > 0.0f) {
+      const double k = c * c * static_cast<double>(len) * len * (1.0 - 1e-5);
+      if (k >= 0x1p-40 && k <= 0x1p40) a->sky_pre_k = static_cast<float>(k);
+    }
   }
   if (st != RT4_OK) return st;
   // flat primitive table (rt4_aux.h)
@@ -741,7 +819,7 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess && (flags & RT4_FLAG_SAMPLER_LUT)) {
-    e = hipMalloc(&c->d_wlut, sizeof(float) << 23);
+    e = hipMalloc(&c->d_wlut, sizeof(WEntry) << 23);
     if (e == hipSuccess) {
       hipLaunchKernelGGL(rt4_build_wlut_kernel, dim3((1u << 23) / 256), dim3(256), 0, 0, c->d_wlut);
       e = hipGetLastError();

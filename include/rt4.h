@@ -248,7 +248,7 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
 int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* err, size_t errlen);
 void rt4_context_destroy(rt4_context* ctx);
 
-/* Pixel set of one launch. Local row i in [0,h) maps to image row
+/* Pixel set of one launch (w <= 65535, h <= 32767). Local row i in [0,h) maps to image row
  *   band_rows == 0 : y0 + i
  *   band_rows  > 0 : y0 + (i / band_rows) * band_step + (i % band_rows)
  * and local column j in [0,w) to image column x0 + j. Scene coordinates come from the full image
