@@ -15,6 +15,9 @@
 
 namespace rt4 {
 
+typedef float f8v __attribute__((ext_vector_type(8)));    // one s_load_dwordx8 when wave-uniform
+typedef float f16v __attribute__((ext_vector_type(16)));  // one s_load_dwordx16
+
 struct DivC {
   float b;       // divisor
   float y;       // RN(1/b)
@@ -50,9 +53,23 @@ constexpr int MAX_PRIMS = RT4_MAX_SPACES + RT4_MAX_SPHERES + RT4_MAX_CYLINDERS +
 // P >= r^2 (1 + 7e-7) + 3.1e-7 d2 suffices, which the test exceeds ~13x (d2 term) / ~140x (r^2).
 // Culled spheres are exactly the ones the exact path reports as no hit, so results are unchanged.
 constexpr float SPHERE_CULL_K = 4e-6f;
-struct SphereCull {
-  float d2_out;  // smallest d2 with RN(sqrt(d2)) >= max(r, SMALL_F)
-  float r2m;     // RN(r^2 (1 + 1e-4)); +inf disables the cull (tiny or non-finite r)
+// Everything the cull pass reads per sphere, in one 32-B block (one wide scalar load per sphere pair
+// instead of one load and one wait per field).
+struct alignas(32) SphereCull {
+  float center[4];  // spheres[i].center
+  float d2_out;     // smallest d2 with RN(sqrt(d2)) >= max(r, SMALL_F)
+  float r2m;        // RN(r^2 (1 + 1e-4)); +inf disables the cull (tiny or non-finite r)
+  float pad[2];
+};
+
+// Everything final_light reads on its common paths (constant override, sky pre-test), in one 64-B block.
+struct alignas(64) HotSky {
+  float sky[3];        // sky_light (shader.frag:405)
+  float pre_k;         // sky_pre_k below
+  float sun_drct[4];   // sun.drct
+  float const_rgb[3];  // final_light_const (RT4_FINAL_LIGHT_CONSTANT)
+  int32_t mode;        // final_light_mode
+  float pad[4];
 };
 
 struct SceneAux {
@@ -76,6 +93,7 @@ struct SceneAux {
                      // a = dot(drct, sun.drct), l2 = dot(drct, drct) in [2^-40, 2^40] implies
                      // v_cos <= sky_c_star. sky_pre_k = RN(c*^2 len(sun)^2 (1 - 1e-5)); 0 disables.
   int32_t pad2_[2];
+  HotSky hot_sky;
   SphereCull sphere_cull[RT4_MAX_SPHERES];
   PrimEntry prims[MAX_PRIMS];
 };

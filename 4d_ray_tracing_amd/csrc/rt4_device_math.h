@@ -40,7 +40,32 @@ __device__ __forceinline__ V4 mad(V4 a, float s, V4 c) {  // a*s + c
 __device__ __forceinline__ float dot(V4 a, V4 b) {
   return fmaf_(a.w, b.w, fmaf_(a.z, b.z, fmaf_(a.y, b.y, a.x * b.x)));
 }
-__device__ __forceinline__ float length(V4 v) { return __builtin_sqrtf(dot(v, v)); }
+#ifndef RT4_FAST_SQRT
+#define RT4_FAST_SQRT 1
+#endif
+// Correctly rounded sqrt: the same value as __builtin_sqrtf under -fhip-fp32-correctly-rounded-divide-sqrt,
+// minus the library expansion's input scaling and class fix-up when no lane needs them. For |x|
+// outside (0, 2^-96) the hardware estimate v_sqrt_f32 plus the one-ulp residual correction of that expansion is
+// already the correctly rounded result (+-0, +inf, NaN and negative inputs included); inside, the
+// library path runs. Verified against __builtin_sqrtf on all 2^32 inputs (rt4_debug_verify_sqrt).
+__device__ __forceinline__ float sqrt_core(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rdn = fmaf_(-sdn, s, x);
+  const float rup = fmaf_(-sup, s, x);
+  const float r = rdn <= 0.0f ? sdn : s;
+  return rup > 0.0f ? sup : r;
+}
+__device__ __forceinline__ float sqrt_(float x) {
+#if RT4_FAST_SQRT
+  // |x| in (0, 2^-96), denormals included, tested on the bit pattern: float compares may see a
+  // denormal as zero
+  if ((__float_as_uint(x) & 0x7FFFFFFFu) - 1u >= 0x0F7FFFFFu) return sqrt_core(x);
+#endif
+  return __builtin_sqrtf(x);
+}
+__device__ __forceinline__ float length(V4 v) { return sqrt_(dot(v, v)); }
 
 // ---- transcendentals ------------------------------------------------------------------------
 __device__ __forceinline__ float asin_core(float s, float z) {
@@ -55,7 +80,7 @@ __device__ __forceinline__ float asin_(float x) {
   bool big = a > 0.5f;
   float zb = 0.5f * (1.0f - a);
   float z = big ? zb : a * a;
-  float s = big ? __builtin_sqrtf(zb) : a;
+  float s = big ? sqrt_(zb) : a;
   float c = asin_core(s, z);
   float r = big ? (PIO2_F - 2.0f * c) : c;
   return __builtin_copysignf(r, x);
@@ -66,7 +91,7 @@ __device__ __forceinline__ float acos_(float x) {
   bool big = a > 0.5f;
   float zb = 0.5f * (1.0f - a);
   float z = big ? zb : x * x;
-  float s = big ? __builtin_sqrtf(zb) : x;
+  float s = big ? sqrt_(zb) : x;
   float c = asin_core(s, z);
   float t = 2.0f * c;
   float rb = x > 0.0f ? t : PI_F - t;
@@ -124,7 +149,7 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {  // :94-102
 
 // ---- S^3 sampler (shader.frag:136-150) ------------------------------------------------------------
 __device__ __forceinline__ float volume_by_w(float w) {  // :136-138
-  return (w * __builtin_sqrtf(1.0f - w * w) - acos_(w)) / PI_F + 1.0f;
+  return (w * sqrt_(1.0f - w * w) - acos_(w)) / PI_F + 1.0f;
 }
 __device__ __forceinline__ float w_by_volume(float v, int* iters) {  // :141-150
   float old_w;

@@ -68,7 +68,7 @@ __device__ __forceinline__ Cand sphere_cand(V4 center, float r, const DivC& dc, 
   const bool flip = outer && len_po > r;
   if (flip) angle_oap = PI_F - angle_oap;
   const float angle_aop = PI_F - angle_opa - angle_oap;
-  const float dist = __builtin_sqrtf(r * r + len_po * len_po - 2.0f * r * len_po * cos_(angle_aop));
+  const float dist = sqrt_(r * r + len_po * len_po - 2.0f * r * len_po * cos_(angle_aop));
   return Cand{true, flip, dist, dist, id};
 }
 
@@ -107,11 +107,11 @@ __device__ __forceinline__ void sphere_dist2(const SphereCore2& c, float r, floa
   {
     const float oap = flip_outer ? PI_F - c.angle_oap : c.angle_oap;
     const float aop = PI_F - c.angle_opa - oap;
-    d_outer = __builtin_sqrtf(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(aop));
+    d_outer = sqrt_(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(aop));
   }
   if (flip_outer) {  // outer = false never flips
     const float aop = PI_F - c.angle_opa - c.angle_oap;
-    d_inner = __builtin_sqrtf(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(aop));
+    d_inner = sqrt_(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(aop));
   } else {
     d_inner = d_outer;  // identical op sequence when no flip
   }
@@ -147,12 +147,11 @@ __device__ __forceinline__ float axes_dist_sq(float dist, const Ray& ray, V4 cp,
 }
 
 __device__ __forceinline__ Cand union_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                           int i, const Ray& ray) {  // :284-294
+                                           int i, uint32_t base, const Ray& ray) {  // :284-294
   const rt4_cylinders_union& u = S->unions[i];
   const V4 p1 = ld4(u.cylinder1.point), a11 = ld4(u.cylinder1.axis1), a12 = ld4(u.cylinder1.axis2);
   const V4 p2 = ld4(u.cylinder2.point), a21 = ld4(u.cylinder2.axis1), a22 = ld4(u.cylinder2.axis2);
   const float gt = X->union_gt[i];
-  const uint32_t base = static_cast<uint32_t>(X->base_union + 2 * i);
   Cand c1 = cyl_cand(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], true, base);
   if (c1.hit && axes_dist_sq(c1.dist, ray, p2, a21, a22) > gt) c1.hit = false;
   Cand c2 = cyl_cand(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], true, base + 1);
@@ -203,11 +202,10 @@ __device__ __forceinline__ Cand tiger_pair(V4 cp, V4 a1, V4 a2, float r_in, floa
 }
 
 __device__ __forceinline__ Cand tiger_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                           int i, const Ray& ray) {  // :327-341
+                                           int i, uint32_t base, const Ray& ray) {  // :327-341
   const rt4_tiger& t = S->tigers[i];
   const V4 pA = ld4(t.inner_cyl1.point), a1 = ld4(t.inner_cyl1.axis1), a2 = ld4(t.inner_cyl1.axis2);
   const V4 pB = ld4(t.inner_cyl2.point), a3 = ld4(t.inner_cyl2.axis1), a4 = ld4(t.inner_cyl2.axis2);
-  const uint32_t base = static_cast<uint32_t>(X->base_tiger + 4 * i);
   const Cand lo = tiger_pair(pA, a1, a2, t.inner_cyl1.r, t.outer_cyl1.r, X->tiger_r[i][0], X->tiger_r[i][1], pB, a3,
                              a4, X->tiger_gt[i][0], X->tiger_lt[i][0], ray, base);
   const Cand hi = tiger_pair(pB, a3, a4, t.inner_cyl2.r, t.outer_cyl2.r, X->tiger_r[i][2], X->tiger_r[i][3], pA, a1,
@@ -229,10 +227,9 @@ __device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uin
   return Cand{true, false, dist, 0.0f, id};
 }
 
-__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                               int i, const Ray& ray) {  // :394-400
+__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, int i, uint32_t base,
+                                               const Ray& ray) {  // :394-400
   const rt4_hypercube& hc = S->hypercubes[i];
-  const uint32_t base = static_cast<uint32_t>(X->base_cube + 8 * i);
   Cand res = no_cand();
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -266,11 +263,32 @@ __device__ __forceinline__ void for_count(int runtime_n, F&& body) {
   }
 }
 
+// Flat primitive-table index of each group's first entry (rt4_aux.h SceneAux::prims order): compile-time
+// for exact-count shapes (the scene-shape check pins one union / hypercube / tiger), else read.
+struct PrimBases {
+  uint32_t sphere, cyl, uni, cube, tiger;
+};
+template <uint32_t SH>
+__device__ __forceinline__ PrimBases prim_bases(const SceneAux* __restrict__ X) {
+  constexpr uint32_t K = SH & 0xFFu;
+  constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2), NCY = sh_count(SH, 3);
+  if constexpr (NSP != 0 && NSH != 0 && NCY != 0) {
+    constexpr uint32_t sph = NSP - 1, cyl = sph + NSH - 1, uni = cyl + NCY - 1;
+    constexpr uint32_t cube = uni + ((K & K_UNION) ? 2u : 0u), tiger = cube + ((K & K_HYPERCUBE) ? 8u : 0u);
+    return PrimBases{sph, cyl, uni, cube, tiger};
+  } else {
+    return PrimBases{static_cast<uint32_t>(X->base_sphere), static_cast<uint32_t>(X->base_cyl),
+                     static_cast<uint32_t>(X->base_union), static_cast<uint32_t>(X->base_cube),
+                     static_cast<uint32_t>(X->base_tiger)};
+  }
+}
+
 template <uint32_t SH>
 __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
                                           const PrimEntry* P, const Ray& ray) {
   constexpr uint32_t K = SH & 0xFFu;
   constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2), NCY = sh_count(SH, 3);
+  const PrimBases B = prim_bases<SH>(X);
   Cand inter = no_cand();
   if (K & K_SPACES) for_count<NSP>(S->n_spaces, [&](int i) { inter = closest(space_cand(S, i, ray), inter); });
   if (K & K_SPHERES) {
@@ -282,18 +300,18 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
     // error bound that makes the cull exact).
     uint32_t pend = 0;
     for_count<NSH>(S->n_spheres, [&](int i) {
-      const V4 po = sub(ld4(S->spheres[i].center), ray.point);
+      const f8v k = *reinterpret_cast<const f8v*>(&X->sphere_cull[i]);  // one 32-B scalar load
+      const V4 po = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
       const float d2 = dot(po, po);  // exactly the dot whose sqrt is len_po in sphere_cand
       const float dp = dot(po, ray.drct);
-      const SphereCull& k = X->sphere_cull[i];
-      const bool outside = d2 >= k.d2_out;  // len_po >= max(r, SMALL)
-      const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k.r2m));
+      const bool outside = d2 >= k[4];  // len_po >= max(r, SMALL)
+      const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5]));
       pend |= skip ? 0u : (1u << i);
     });
     while (pend) {
       const int i = __builtin_ctz(pend);
       pend &= pend - 1u;
-      const uint32_t id = static_cast<uint32_t>(X->base_sphere + i);
+      const uint32_t id = B.sphere + static_cast<uint32_t>(i);
       const PrimEntry& e = P[id];
       const DivC dc{e.r, e.y, e.fast, 0};
       inter = closest(sphere_cand(ld4(e.p), e.r, dc, ray, true, id), inter);
@@ -302,7 +320,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
     for_count<NSH>(S->n_spheres, [&](int i) {
       const rt4_sphere& sp = S->spheres[i];
       inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true,
-                                  static_cast<uint32_t>(X->base_sphere + i)),
+                                  B.sphere + static_cast<uint32_t>(i)),
                       inter);
     });
 #endif
@@ -312,12 +330,12 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
       const rt4_cylinder& c = S->cylinders[i];
       const V4 cp = ld4(c.point);
       inter = closest(cyl_cand(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], true,
-                               static_cast<uint32_t>(X->base_cyl + i)),
+                               B.cyl + static_cast<uint32_t>(i)),
                       inter);
     });
-  if (K & K_UNION) inter = closest(union_cand(S, X, 0, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, X, 0, ray), inter);
-  if (K & K_TIGER) inter = closest(tiger_cand(S, X, 0, ray), inter);
+  if (K & K_UNION) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, 0, B.cube, ray), inter);
+  if (K & K_TIGER) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
   return inter;
 }
 

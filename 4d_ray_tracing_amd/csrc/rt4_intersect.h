@@ -87,7 +87,7 @@ __device__ __forceinline__ Hit sphere_finish(const SphereCore& c, V4 center, flo
   const bool flip = outer && c.len_po > r;
   const float angle_oap = flip ? PI_F - c.angle_oap : c.angle_oap;
   const float angle_aop = PI_F - c.angle_opa - angle_oap;
-  const float dist = __builtin_sqrtf(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(angle_aop));
+  const float dist = sqrt_(r * r + c.len_po * c.len_po - 2.0f * r * c.len_po * cos_(angle_aop));
   V4 norm = divs(sub(center, mad(ray.drct, dist, ray.point)), r);
   if (flip) norm = neg(norm);
   Hit h{!c.miss, dist, norm, mat};

@@ -131,16 +131,17 @@ struct Finder<GENERIC> {
 // ---------------------------------------------------------------- shading (shader.frag:404-495)
 __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
                                          V4 drct) {  // :454-468
-  if (S->final_light_mode == RT4_FINAL_LIGHT_CONSTANT) return ld3(S->final_light_const);
-  V3 sky = ld3(S->sky_light);
-  V4 sd = ld4(S->sun.drct);
+  const f16v h = *reinterpret_cast<const f16v*>(&X->hot_sky);  // rt4_aux.h HotSky: one wide scalar load
+  if (__float_as_int(h[11]) == RT4_FINAL_LIGHT_CONSTANT) return V3{h[8], h[9], h[10]};
+  const V3 sky{h[0], h[1], h[2]};
+  const V4 sd{h[4], h[5], h[6], h[7]};
   const float a_ds = dot(drct, sd), l2 = dot(drct, drct);
 #if RT4_SKY_PRETEST
   // clearly away from the sun: the exact v_cos below would be <= sky_c_star (rt4_aux.h sky_pre_k)
-  if (l2 >= 0x1p-40f && l2 <= 0x1p40f && (a_ds <= 0.0f || a_ds * a_ds < l2 * X->sky_pre_k)) return sky;
+  if (l2 >= 0x1p-40f && l2 <= 0x1p40f && (a_ds <= 0.0f || a_ds * a_ds < l2 * h[3])) return sky;
 #endif
   // angle(), :45-50: (dot / length(drct)) / length(sun.drct); the second length is a scene constant
-  const float vcos = div_c(a_ds / __builtin_sqrtf(l2), X->sun_len);
+  const float vcos = div_c(a_ds / sqrt_(l2), X->sun_len);
   float ang = S->sun.angular_size;
 #if RT4_SKY_THRESHOLD
   if (!(vcos > X->sky_c_star)) return sky;  // acos(vcos) >= ang (or NaN): the sky branch, exactly
@@ -191,14 +192,14 @@ __device__ __forceinline__ V4 rand_drct(RngState& rng, const WEntry* __restrict_
 #if RT4_LUT2
     r = e.y;  // = sqrt(1 - w*w) with the same ops, tabulated (rt4_build_wlut_kernel)
 #else
-    r = __builtin_sqrtf(1.0f - w * w);
+    r = sqrt_(1.0f - w * w);
 #endif
   } else {
     w = w_by_volume(rand_(rng), nullptr);
-    r = __builtin_sqrtf(1.0f - w * w);
+    r = sqrt_(1.0f - w * w);
   }
   const float z = (rand_(rng) * 2.0f - 1.0f) * r;
-  const float rr = __builtin_sqrtf(r * r - z * z);
+  const float rr = sqrt_(r * r - z * z);
   const float fi = rand_(rng) * 2.0f * PI_F;
   float sf, cf;
   sincos_(fi, sf, cf);
@@ -439,7 +440,7 @@ __global__ void rt4_build_wlut_kernel(WEntry* __restrict__ lut) {
   if (m >= (1u << 23)) return;
   const float w = w_by_volume(__uint_as_float(m | 0x3F800000u) - 1.0f, nullptr);
 #if RT4_LUT2
-  lut[m] = make_float2(w, __builtin_sqrtf(1.0f - w * w));
+  lut[m] = make_float2(w, sqrt_(1.0f - w * w));
 #else
   lut[m] = w;
 #endif
@@ -458,6 +459,18 @@ __global__ void rt4_verify_div_kernel(float b, float y, unsigned* __restrict__ m
     bad += same ? 0u : 1u;
   }
   if (bad) atomicAdd(mismatches, bad);
+}
+
+// Exhaustive check of sqrt_ (rt4_device_math.h) against the IEEE square root for every 32-bit pattern.
+__global__ void rt4_verify_sqrt_kernel(unsigned long long* __restrict__ mismatches) {
+  unsigned bad = 0;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+    const float x = __uint_as_float(static_cast<uint32_t>(i));
+    const float a = sqrt_(x), b = __builtin_sqrtf(x);
+    bad += (__float_as_uint(a) == __float_as_uint(b) || (a != a && b != b)) ? 0u : 1u;
+  }
+  if (bad) atomicAdd(mismatches, static_cast<unsigned long long>(bad));
 }
 
 // min over all float patterns c with acos_(c) < ang, as an order-preserving key (0xFFFFFFFF: none)
@@ -490,6 +503,7 @@ __global__ void rt4_eval_kernel(int fn, const float* __restrict__ in, float* __r
     case RT4_EVAL_VOLUME_BY_W: r = volume_by_w(x); break;
     case RT4_EVAL_W_BY_VOLUME: r = w_by_volume(x, &it); break;
     case RT4_EVAL_HASH: r = __uint_as_float(hash_u32(__float_as_uint(x))); break;
+    case RT4_EVAL_SQRT: r = sqrt_(x); break;
     default: r = __builtin_nanf(""); break;
   }
   out[t] = r;
@@ -595,8 +609,12 @@ uint32_t scene_shape(const rt4_scene_desc& s) {
                            (static_cast<uint32_t>(s.n_spheres + 1) << 16) |
                            (static_cast<uint32_t>(s.n_cylinders + 1) << 24);
 #ifndef RT4_NO_EXACT_COUNTS  // A/B knob: -DRT4_NO_EXACT_COUNTS runs every scene on its runtime-count kernel
-  for (const Variant& v : kVariants)  // exact counts first (unrolled), then the runtime-count kernel
-    if (v.shape == counted) return counted;
+  // exact counts first (unrolled; primitive-table bases compile-time, rt4_fast.h prim_bases: objects of
+  // an untested group would shift them), then the runtime-count kernel
+  const bool bases_fixed = s.n_unions == ((k & K_UNION) ? 1 : 0) && s.n_hypercubes == ((k & K_HYPERCUBE) ? 1 : 0) &&
+                           s.n_tigers == ((k & K_TIGER) ? 1 : 0);
+  for (const Variant& v : kVariants)
+    if (bases_fixed && v.shape == counted) return counted;
 #endif
   for (const Variant& v : kVariants)
     if (v.shape == k) return k;
@@ -695,6 +713,7 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
   for (int i = 0; i < s.n_spheres && st == RT4_OK; i++) st = make_divc(ctx, s.spheres[i].r, &a->sphere_r[i], err, errlen);
   for (int i = 0; i < s.n_spheres; i++) {  // rt4_aux.h SphereCull
     const float r = s.spheres[i].r;
+    std::memcpy(a->sphere_cull[i].center, s.spheres[i].center, sizeof a->sphere_cull[i].center);
     a->sphere_cull[i].d2_out = sqrt_lt_threshold(std::max(r, 0.0003f));  // SMALL_F, shader.frag:24
     const bool ok = r >= 1e-15f && r <= 1e15f;  // r <= 0: sin_oap < 1 always, never cull
     a->sphere_cull[i].r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
@@ -749,6 +768,12 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     }
   }
   if (st != RT4_OK) return st;
+  HotSky& hs = a->hot_sky;  // rt4_aux.h HotSky
+  std::memcpy(hs.sky, s.sky_light, sizeof hs.sky);
+  hs.pre_k = a->sky_pre_k;
+  std::memcpy(hs.sun_drct, s.sun.drct, sizeof hs.sun_drct);
+  std::memcpy(hs.const_rgb, s.final_light_const, sizeof hs.const_rgb);
+  hs.mode = s.final_light_mode;
   // flat primitive table (rt4_aux.h)
   int n = 0;
   auto add = [&](int kind, const float* p, const float* a1, const float* a2, float r, const DivC& dc,
@@ -956,6 +981,24 @@ int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_
     rt4_set_err(err, errlen, "debug_eval failed: %s", hipGetErrorString(e));
     return RT4_ERR_HIP;
   }
+  return RT4_OK;
+}
+
+int rt4_debug_verify_sqrt(rt4_context* ctx, uint64_t* mismatches, char* err, size_t errlen) {
+  if (!ctx || !mismatches) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  HIP_TRY(hipSetDevice(ctx->device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, sizeof(unsigned long long));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(rt4_verify_sqrt_kernel, dim3(65536), dim3(256), 0, 0, d);
+    e = hipGetLastError();
+  }
+  unsigned long long v = 0;
+  if (e == hipSuccess) e = hipMemcpy(&v, d, sizeof v, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return rt4_set_err(err, errlen, "verify_sqrt failed: %s", hipGetErrorString(e)), RT4_ERR_HIP;
+  *mismatches = v;
   return RT4_OK;
 }
 

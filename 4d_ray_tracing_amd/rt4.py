@@ -74,7 +74,7 @@ FINAL_LIGHT_SUN_SKY, FINAL_LIGHT_CONSTANT = 0, 1
 SECTION_YXZ, SECTION_YWZ, SECTION_YXW = 0, 1, 2
 FLAG_SAMPLER_LUT = 0x1
 FLAG_GENERIC_KERNEL = 0x2
-EVAL_ACOS, EVAL_ASIN, EVAL_SIN, EVAL_COS, EVAL_VOLUME_BY_W, EVAL_W_BY_VOLUME, EVAL_HASH = range(7)
+EVAL_ACOS, EVAL_ASIN, EVAL_SIN, EVAL_COS, EVAL_VOLUME_BY_W, EVAL_W_BY_VOLUME, EVAL_HASH, EVAL_SQRT = range(8)
 
 
 class SceneDesc(Structure):
@@ -160,6 +160,7 @@ def _load():
         "rt4_debug_eval": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64] + E, c_int),
         "rt4_debug_find_intersection": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int64] + E, c_int),
         "rt4_context_kernel_shape": ([c_void_p], c_uint32),
+        "rt4_debug_verify_sqrt": ([c_void_p, POINTER(c_uint64)] + E, c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)  # AttributeError if the library lacks a declared export
@@ -175,7 +176,7 @@ EXPORTED = (
     "rt4_properties_get_float rt4_properties_get_bool rt4_orientation_update rt4_section_basis "
     "rt4_uniforms_from_properties rt4_window_cells rt4_scene_load_frag rt4_scene_parse_frag rt4_scene_validate "
     "rt4_scene_builtin rt4_context_create rt4_context_set_scene rt4_context_destroy rt4_render_device rt4_render_host "
-    "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape"
+    "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -409,6 +410,13 @@ class Tracer:
         _check(lib.rt4_debug_eval(self._h, fn, c_void_p(x.ctypes.data), c_void_p(out.ctypes.data),
                                   c_void_p(aux.ctypes.data), x.size, err, len(err)), err)
         return out, aux
+
+    def debug_verify_sqrt(self) -> int:
+        """Mismatches of the kernel's sqrt against IEEE sqrt over all 2^32 inputs (rt4.h)."""
+        n = c_uint64(0)
+        err = _errbuf()
+        _check(lib.rt4_debug_verify_sqrt(self._h, ctypes.byref(n), err, len(err)), err)
+        return n.value
 
     def debug_find_intersection(self, rays):
         import numpy as np

@@ -278,7 +278,8 @@ enum rt4_eval_fn {
   RT4_EVAL_ACOS = 0, RT4_EVAL_ASIN = 1, RT4_EVAL_SIN = 2, RT4_EVAL_COS = 3,
   RT4_EVAL_VOLUME_BY_W = 4, /* shader.frag:136-138 */
   RT4_EVAL_W_BY_VOLUME = 5, /* shader.frag:141-150; aux[i] = Newton iterations */
-  RT4_EVAL_HASH = 6         /* shader.frag:94-102 on the bit pattern of in[i] */
+  RT4_EVAL_HASH = 6,        /* shader.frag:94-102 on the bit pattern of in[i] */
+  RT4_EVAL_SQRT = 7         /* the kernel's correctly rounded sqrt (GLSL sqrt, e.g. :47, :137, :216) */
 };
 /* Evaluates a device math function element-wise (synchronous; host buffers). */
 int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_t* aux, int64_t n, char* err,
@@ -289,6 +290,10 @@ int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_
  * glow, refl_prob}; out_color: n x 3 floats. Synchronous; host buffers. */
 int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out, float* out_color, int64_t n,
                                 char* err, size_t errlen);
+
+/* Counts the 32-bit patterns x for which the kernel's sqrt (fast path without input scaling) differs
+ * from the IEEE square root; 0 expected. Exhaustive over all 2^32 inputs on the device (~10 ms). */
+int rt4_debug_verify_sqrt(rt4_context* ctx, uint64_t* mismatches, char* err, size_t errlen);
 
 /* Trace kernel selected for the context's scene: 0xFFFFFFFF = the generic find_intersection
  * (any group list); otherwise the K_* group bits (low byte: 1 spaces, 2 spheres, 4 cylinders,

@@ -48,6 +48,24 @@ def test_device_math_bitwise(tracer, rt4, oracle):
         assert_bits(g, c, f"eval fn {fn}")
 
 
+def test_sqrt_exhaustive(tracer, rt4):
+    """The kernel's sqrt (fast path without input scaling, rt4_device_math.h sqrt_) equals the IEEE
+    square root on every one of the 2^32 float patterns (device-side sweep)."""
+    assert tracer.debug_verify_sqrt() == 0
+
+
+def test_sqrt_values(tracer, rt4):
+    rng = np.random.default_rng(5)
+    bits = rng.integers(0, 2**32, 400000, dtype=np.uint64).astype(np.uint32)
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, 1e-40, 2.0**-96, 2.0**-97, 3.4e38, -1.0, 2.0, 0.25],
+                       np.float32)
+    x = np.concatenate([bits.view(np.float32), special])
+    g, _ = tracer.debug_eval(rt4.EVAL_SQRT, x)
+    with np.errstate(invalid="ignore"):
+        ref = np.sqrt(x)
+    assert_bits(g, ref, "sqrt_")
+
+
 def test_hash_bitwise(tracer, rt4, oracle):
     x = np.random.default_rng(2).integers(0, 2**32, 100000, dtype=np.uint64).astype(np.uint32).view(np.float32)
     g, _ = tracer.debug_eval(rt4.EVAL_HASH, x)

@@ -33,7 +33,10 @@ elif [ "$cmd" = run ]; then
   for r in $(seq 1 "$rounds"); do
     for so in "$VDIR"/*.so; do
       name=$(basename "$so" .so)
-      out=$(RT4_LIB=$so timeout -k 10 300 python "$ROOT/bench.py" $args 2>/dev/null | tail -1)
+      errf=$(mktemp)
+      out=$(RT4_LIB=$so timeout -k 10 300 python "$ROOT/bench.py" $args 2>"$errf" | tail -1)
+      if [ -z "$out" ]; then echo "$name: bench failed:"; tail -5 "$errf"; rm -f "$errf"; continue; fi
+      rm -f "$errf"
       python3 - "$name" "$out" <<'PY'
 import json, sys
 d = json.loads(sys.argv[2])
