@@ -322,6 +322,24 @@ int rt4_abi_version(void) { return RT4_ABI_VERSION; }
 size_t rt4_scene_desc_size(void) { return sizeof(rt4_scene_desc); }
 size_t rt4_uniforms_size(void) { return sizeof(rt4_uniforms); }
 
+int32_t rt4_frame_format_bytes(int32_t format) {
+  switch (format) {
+    case RT4_FRAME_RGBA32F: return 16;
+    case RT4_FRAME_RGBA16F: return 8;
+    case RT4_FRAME_RGBA8: return 4;
+    default: return 0;
+  }
+}
+
+int rt4_progressive_uniforms(const rt4_uniforms* base, uint32_t frame_number, rt4_uniforms* out) {
+  if (!base || !out || frame_number == 0) return RT4_ERR_ARG;
+  rt4_uniforms u = *base;
+  u.part = 1.0f / static_cast<float>(frame_number);  // main.cpp:87 (frameNumber is unsigned, 1.0f / n in fp32)
+  u.seed = static_cast<int32_t>(static_cast<uint32_t>(base->seed) ^ (frame_number * 0x9E3779B9u));
+  *out = u;
+  return RT4_OK;
+}
+
 const char* rt4_build_info(void) {
   return "rt4 0.1 target=gfx950 fp32-contract=off div/sqrt=correctly-rounded built " __DATE__;
 }
@@ -335,9 +353,9 @@ int rt4_check_render_args(const rt4_uniforms* u, const rt4_region* r, long long 
   if (r->band_rows < 0 || (r->band_rows > 0 && r->band_step < r->band_rows))
     return rt4_set_err(err, errlen, "bad band layout (band_rows %d, band_step %d)", r->band_rows, r->band_step),
            RT4_ERR_ARG;
-  // the kernel packs a region-local pixel as j | i << 16 (rt4_trace.hip, RT4_COLD_LDS)
-  if (r->w > 65535 || r->h > 32767)
-    return rt4_set_err(err, errlen, "region too large (%d x %d; at most 65535 x 32767)", r->w, r->h), RT4_ERR_ARG;
+  // the kernel packs a region-local pixel as j | i << 16 | job << 30 (rt4_trace.hip pack_pixel)
+  if (r->w > 65535 || r->h > 16383)
+    return rt4_set_err(err, errlen, "region too large (%d x %d; at most 65535 x 16383)", r->w, r->h), RT4_ERR_ARG;
   if (u->samples < 0 || u->reflections_amount < 0)
     return rt4_set_err(err, errlen, "samples/reflections_amount must be >= 0"), RT4_ERR_ARG;
   if (!(u->resolution[0] > 0.0f) || !(u->resolution[1] > 0.0f))

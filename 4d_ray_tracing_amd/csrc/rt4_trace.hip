@@ -56,9 +56,6 @@ __device__ __forceinline__ float went_w(WEntry e) { return e.x; }
 using WEntry = float;
 __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #endif
-#ifndef RT4_COLD_LDS
-#define RT4_COLD_LDS 1  // per-lane state touched once per sample (d0, light sum, pixel) lives in LDS
-#endif
 #ifndef RT4_SKY_PRETEST
 #define RT4_SKY_PRETEST 1
 #endif
@@ -206,44 +203,84 @@ __device__ __forceinline__ V4 rand_drct(RngState& rng, const WEntry* __restrict_
   return V4{rr * cf, rr * sf, z, w};
 }
 
-struct KernelArgs {
-  rt4_uniforms u;
+// One image of a launch: the whole frame, or one section of ThreeWindowGroup (rt4_render_sections_device).
+struct JobArgs {
+  float resolution[2], mtr_sizes[2];
+  float vec_to_mtr[4], top_drct[4], right_drct[4];
   rt4_region reg;
+  void* frame;
   int64_t row_stride_px;
+  unsigned tile_base;  // first queue tile of the job (8x8 tiles, row-major inside the job)
+  unsigned tiles_x;
+};
+struct KernelArgs {
+  // uniforms every job shares (one shader, one frame: rt4_check_jobs)
+  int32_t seed, samples, reflections_amount;
+  float small_indent, part, k;  // k = light_to_color_conversion_coefficient
+  float focus[4];
+  int32_t format, n_jobs;
+  unsigned total;  // 64 x tiles of all jobs
+  JobArgs jobs[RT4_MAX_SECTIONS];
 };
 
 __device__ __forceinline__ int region_row(const rt4_region& r, int i) {
   return r.band_rows > 0 ? r.y0 + (i / r.band_rows) * r.band_step + (i % r.band_rows) : r.y0 + i;
 }
 
-// light /= samples; light_to_color; mix(old_frame, new, part); alpha 1 (shader.frag:522-527)
-__device__ __forceinline__ void write_pixel(const KernelArgs& a, float4* __restrict__ frame, int j, int i, V3 light) {
-  const float ns = static_cast<float>(a.u.samples);
+// A lane's pixel, packed into one dword of its cold state: region-local j (16 bits) | i (14) | job (2).
+__device__ __forceinline__ int pack_pixel(int j, int i, int job) { return j | (i << 16) | (job << 30); }
+
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+
+// light /= samples; light_to_color; mix(old_frame, new, part); alpha 1 (shader.frag:522-527), in the
+// launch's frame format (rt4.h rt4_frame_format; the blend is fp32 in every format)
+__device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& J, int pk, V3 light) {
+  const int j = pk & 0xFFFF, i = (pk >> 16) & 0x3FFF;
+  const float ns = static_cast<float>(a.samples);
   light = V3{light.x / ns, light.y / ns, light.z / ns};
-  const float k = a.u.light_to_color_conversion_coefficient;
+  const float k = a.k;
   const V3 c{1.0f - 1.0f / fmaf_(k, light.x, 1.0f), 1.0f - 1.0f / fmaf_(k, light.y, 1.0f),
              1.0f - 1.0f / fmaf_(k, light.z, 1.0f)};
-  float4* px = frame + static_cast<int64_t>(i) * a.row_stride_px + j;
-  const float4 old = *px;
-  const float part = a.u.part, keep = 1.0f - a.u.part;
-  *px = make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep), fmaf_(c.z, part, old.z * keep),
-                    1.0f);
+  const float part = a.part, keep = 1.0f - a.part;
+  char* base = static_cast<char*>(J.frame);
+  const int64_t at = static_cast<int64_t>(i) * J.row_stride_px + j;
+  if (a.format == RT4_FRAME_RGBA16F) {
+    h4v* px = reinterpret_cast<h4v*>(base) + at;
+    const h4v o = *px;
+    h4v v;
+    v[0] = static_cast<_Float16>(fmaf_(c.x, part, static_cast<float>(o[0]) * keep));
+    v[1] = static_cast<_Float16>(fmaf_(c.y, part, static_cast<float>(o[1]) * keep));
+    v[2] = static_cast<_Float16>(fmaf_(c.z, part, static_cast<float>(o[2]) * keep));
+    v[3] = static_cast<_Float16>(1.0f);
+    *px = v;
+  } else if (a.format == RT4_FRAME_RGBA8) {
+    uint32_t* px = reinterpret_cast<uint32_t*>(base) + at;
+    const uint32_t o = *px;
+    const float oc[3] = {static_cast<float>(o & 0xFFu) / 255.0f, static_cast<float>((o >> 8) & 0xFFu) / 255.0f,
+                         static_cast<float>((o >> 16) & 0xFFu) / 255.0f};
+    const float nc[3] = {fmaf_(c.x, part, oc[0] * keep), fmaf_(c.y, part, oc[1] * keep), fmaf_(c.z, part, oc[2] * keep)};
+    uint32_t v = 0xFF000000u;
+    for (int q = 0; q < 3; q++) v |= static_cast<uint32_t>(fminf(fmaxf(nc[q], 0.0f), 1.0f) * 255.0f + 0.5f) << (8 * q);
+    *px = v;
+  } else {
+    float4* px = reinterpret_cast<float4*>(base) + at;
+    const float4 old = *px;
+    *px = make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep), fmaf_(c.z, part, old.z * keep),
+                      1.0f);
+  }
 }
 
 template <uint32_t K, bool LUT>
 __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
-                                                        float4* __restrict__ frame,
                                                         unsigned long long* __restrict__ counter,
                                                         const WEntry* __restrict__ wlut, unsigned* __restrict__ queue) {
   const unsigned lane = threadIdx.x & 63u;
-  const int W = a.reg.w, H = a.reg.h;
-  const unsigned tiles_x = (static_cast<unsigned>(W) + 7u) >> 3;
-  const unsigned total = tiles_x * ((static_cast<unsigned>(H) + 7u) >> 3) * 64u;
-  const V4 focus = ld4(a.u.focus);
-  const float indent = a.u.small_indent;
-  const int R = a.u.reflections_amount, NS = a.u.samples;
-  const uint32_t useed = static_cast<uint32_t>(a.u.seed);
+  const unsigned total = a.total;
+  const V4 focus = ld4(a.focus);
+  const float indent = a.small_indent;
+  const int R = a.reflections_amount, NS = a.samples;
+  const uint32_t useed = static_cast<uint32_t>(a.seed);
   // the primitive table (normals + materials of hits) is read per lane: stage it in LDS once
   __shared__ float4 lds_prims[K == GENERIC ? 1 : n_prims_of(K) * 6];
   if constexpr (K != GENERIC) {
@@ -260,17 +297,11 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   RngState rng{0u, 0u};
   Ray ray{V4{0.0f, 0.0f, 0.0f, 0.0f}, V4{0.0f, 0.0f, 0.0f, 0.0f}};
   V3 acc{0.0f, 0.0f, 0.0f}, T{1.0f, 1.0f, 1.0f};
-#if RT4_COLD_LDS
   // Cold per-lane state in LDS, one float4 column per lane (ds_read/write_b128, conflict-free):
-  // [0] the pixel's primary direction d0, [256] {light sum, pixel j | i << 16}. Touched once per
-  // sample, so the VGPRs go to occupancy instead.
+  // [0] the pixel's primary direction d0, [256] {light sum, pack_pixel()}. Touched once per sample,
+  // so the VGPRs go to occupancy instead (6 -> 7 waves/SIMD on the sphere scene).
   __shared__ float4 lds_cold[2 * 256];
   float4* const cold = lds_cold + threadIdx.x;
-#else
-  int pj = 0, pi = 0;
-  V4 d0{0.0f, 0.0f, 0.0f, 0.0f};
-  V3 light{0.0f, 0.0f, 0.0f};
-#endif
   int s = 0, b = 0;
   uint32_t n_inter = 0;
 
@@ -278,15 +309,14 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;
   RT4_STAMP(t_loop0);
 #endif
-#if RT4_COLD_LDS
+  // writes the finished pixels of the active lanes; one wave-uniform pass per job, so every job's
+  // frame pointer and stride stay scalar (a per-lane select held them in VGPRs: 8 more per lane)
   auto flush_pixel = [&]() {
     const float4 lp = cold[256];
     const int pk = __float_as_int(lp.w);
-    write_pixel(a, frame, pk & 0xFFFF, pk >> 16, V3{lp.x, lp.y, lp.z});
+    for (int jb = 0; jb < a.n_jobs; jb++)
+      if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
   };
-#else
-  auto flush_pixel = [&]() { write_pixel(a, frame, pj, pi, light); };
-#endif
   while (true) {
     RT4_STAMP(t_ph);
     if (!exhausted) {
@@ -313,33 +343,30 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
             b_end = min(base + BATCH, total);
           }
           const unsigned n = min(nidle - got, b_end - b_next);
+          // a 64-pixel batch is one tile of one job: the job is wave-uniform here (scalar loads)
+          const unsigned btile = b_next >> 6;
+          const int job = (a.n_jobs > 1 && btile >= a.jobs[1].tile_base) + (a.n_jobs > 2 && btile >= a.jobs[2].tile_base);
+          const JobArgs& J = a.jobs[job];
           if (!active && rank >= got && rank < got + n) {
             const unsigned idx = b_next + (rank - got);
-            const unsigned tile = idx >> 6, l = idx & 63u;
-            const int jj = static_cast<int>((tile % tiles_x) * 8u + (l & 7u));
-            const int ii = static_cast<int>((tile / tiles_x) * 8u + (l >> 3));
-            if (jj < W && ii < H) {
+            const unsigned tile = (idx >> 6) - J.tile_base, l = idx & 63u;
+            const int jj = static_cast<int>((tile % J.tiles_x) * 8u + (l & 7u));
+            const int ii = static_cast<int>((tile / J.tiles_x) * 8u + (l >> 3));
+            if (jj < J.reg.w && ii < J.reg.h) {
               // main(): scr_coord = gl_FragCoord.xy / resolution (shader.frag:515-516)
-              const float sx = (static_cast<float>(a.reg.x0 + jj) + 0.5f) / a.u.resolution[0];
-              const float sy = (static_cast<float>(region_row(a.reg, ii)) + 0.5f) / a.u.resolution[1];
+              const float sx = (static_cast<float>(J.reg.x0 + jj) + 0.5f) / J.resolution[0];
+              const float sy = (static_cast<float>(region_row(J.reg, ii)) + 0.5f) / J.resolution[1];
               rng = RngState{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ useed, useed};
               // ray_drct(), shader.frag:501-505
-              const float mx = (sx - 0.5f) * a.u.mtr_sizes[0];
-              const float my = (0.5f - sy) * a.u.mtr_sizes[1];
-              V4 dd = mad(ld4(a.u.right_drct), mx, mad(ld4(a.u.top_drct), my, ld4(a.u.vec_to_mtr)));
+              const float mx = (sx - 0.5f) * J.mtr_sizes[0];
+              const float my = (0.5f - sy) * J.mtr_sizes[1];
+              V4 dd = mad(ld4(J.right_drct), mx, mad(ld4(J.top_drct), my, ld4(J.vec_to_mtr)));
               dd = divs(dd, length(dd));
               ray = Ray{focus, dd};
               acc = V3{0.0f, 0.0f, 0.0f};
               T = V3{1.0f, 1.0f, 1.0f};
-#if RT4_COLD_LDS
               cold[0] = make_float4(dd.x, dd.y, dd.z, dd.w);
-              cold[256] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(jj | (ii << 16)));
-#else
-              d0 = dd;
-              pj = jj;
-              pi = ii;
-              light = V3{0.0f, 0.0f, 0.0f};
-#endif
+              cold[256] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(pack_pixel(jj, ii, job)));
               s = 0;
               b = 0;
               active = NS > 0;
@@ -401,15 +428,10 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         end = b > R;
       }
       if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
-#if RT4_COLD_LDS
         const float4 lp = cold[256];
         cold[256] = make_float4(lp.x + acc.x, lp.y + acc.y, lp.z + acc.z, lp.w);
         const float4 c0 = cold[0];
         ray = Ray{focus, V4{c0.x, c0.y, c0.z, c0.w}};
-#else
-        light = V3{light.x + acc.x, light.y + acc.y, light.z + acc.z};
-        ray = Ray{focus, d0};
-#endif
         ++s;
         b = 0;
         acc = V3{0.0f, 0.0f, 0.0f};
@@ -538,7 +560,7 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const Scen
 }
 
 // ---------------------------------------------------------------- kernel table
-typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, float4*, unsigned long long*,
+typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, unsigned long long*,
                         const WEntry*, unsigned*);
 typedef void (*FindFn)(const rt4_scene_desc*, const SceneAux*, const float*, float*, float*, int64_t);
 
@@ -887,49 +909,125 @@ int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* e
 
 uint32_t rt4_context_kernel_shape(const rt4_context* ctx) { return ctx && ctx->has_scene ? ctx->shape : 0u; }
 
-int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
-                      int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err, size_t errlen) {
-  if (!ctx || !u || !region || !d_rgba) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+// The uniforms every job of one launch shares (KernelArgs), compared bit for bit.
+bool same_shared_uniforms(const rt4_uniforms& a, const rt4_uniforms& b) {
+  return a.seed == b.seed && a.samples == b.samples && a.reflections_amount == b.reflections_amount &&
+         std::memcmp(&a.small_indent, &b.small_indent, 4) == 0 && std::memcmp(&a.part, &b.part, 4) == 0 &&
+         std::memcmp(&a.light_to_color_conversion_coefficient, &b.light_to_color_conversion_coefficient, 4) == 0 &&
+         std::memcmp(a.focus, b.focus, sizeof a.focus) == 0;
+}
+
+int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, int32_t format,
+                unsigned long long* d_counter, void* stream, char* err, size_t errlen) {
+  if (!ctx || !jobs) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
   if (!ctx->has_scene) return rt4_set_err(err, errlen, "context has no scene (rt4_context_set_scene)"), RT4_ERR_ARG;
-  int st = rt4_check_render_args(u, region, row_stride_px, err, errlen);
-  if (st != RT4_OK) return st;
-  if (region->w == 0 || region->h == 0) return RT4_OK;
+  if (n_jobs < 1 || n_jobs > RT4_MAX_SECTIONS)
+    return rt4_set_err(err, errlen, "n_jobs %d not in [1, %d]", n_jobs, RT4_MAX_SECTIONS), RT4_ERR_ARG;
+  if (rt4_frame_format_bytes(format) == 0) return rt4_set_err(err, errlen, "unknown frame format %d", format), RT4_ERR_ARG;
   KernelArgs a;
-  a.u = *u;
-  a.reg = *region;
-  a.row_stride_px = row_stride_px;
+  std::memset(&a, 0, sizeof a);
+  const rt4_uniforms& u0 = jobs[0].u;
+  a.seed = u0.seed;
+  a.samples = u0.samples;
+  a.reflections_amount = u0.reflections_amount;
+  a.small_indent = u0.small_indent;
+  a.part = u0.part;
+  a.k = u0.light_to_color_conversion_coefficient;
+  std::memcpy(a.focus, u0.focus, sizeof a.focus);
+  a.format = format;
+  a.n_jobs = n_jobs;
+  unsigned tiles = 0;
+  for (int q = 0; q < RT4_MAX_SECTIONS; q++) a.jobs[q].tile_base = 0xFFFFFFFFu;
+  for (int q = 0; q < n_jobs; q++) {
+    const rt4_section_job& jb = jobs[q];
+    int st = rt4_check_render_args(&jb.u, &jb.region, jb.row_stride_px, err, errlen);
+    if (st != RT4_OK) return st;
+    if (!same_shared_uniforms(jb.u, u0))
+      return rt4_set_err(err, errlen, "job %d: seed/samples/reflections/small_indent/part/k/focus differ from job 0", q),
+             RT4_ERR_ARG;
+    const bool empty = jb.region.w == 0 || jb.region.h == 0;
+    if (!empty && !jb.d_frame) return rt4_set_err(err, errlen, "job %d: NULL frame", q), RT4_ERR_ARG;
+    JobArgs& J = a.jobs[q];
+    std::memcpy(J.resolution, jb.u.resolution, sizeof J.resolution);
+    std::memcpy(J.mtr_sizes, jb.u.mtr_sizes, sizeof J.mtr_sizes);
+    std::memcpy(J.vec_to_mtr, jb.u.vec_to_mtr, sizeof J.vec_to_mtr);
+    std::memcpy(J.top_drct, jb.u.top_drct, sizeof J.top_drct);
+    std::memcpy(J.right_drct, jb.u.right_drct, sizeof J.right_drct);
+    J.reg = jb.region;
+    J.frame = jb.d_frame;
+    J.row_stride_px = jb.row_stride_px;
+    J.tiles_x = empty ? 1u : static_cast<unsigned>((jb.region.w + 7) / 8);
+    const unsigned t = empty ? 0u : J.tiles_x * static_cast<unsigned>((jb.region.h + 7) / 8);
+    J.tile_base = tiles;
+    tiles += t;
+  }
+  if (tiles == 0) return RT4_OK;
+  a.total = tiles * 64u;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const Variant& v = variant_for(ctx->shape);
   const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0];
   // grid: what the device holds at once; later blocks would only find the queue empty
   int per_cu = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), 256, 0));
-  const long long tiles = static_cast<long long>((region->w + 7) / 8) * ((region->h + 7) / 8);
   long long blocks = static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1);
-  if (blocks > (tiles + 3) / 4) blocks = (tiles + 3) / 4;  // >= one tile per wave
+  if (blocks > (static_cast<long long>(tiles) + 3) / 4) blocks = (static_cast<long long>(tiles) + 3) / 4;  // >= one tile per wave
   if (blocks < 1) blocks = 1;
   unsigned* q = ctx->d_queue + (ctx->launch_seq++ % QUEUE_SLOTS);
   HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
-  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a,
-                     reinterpret_cast<float4*>(d_rgba), d_counter, ctx->d_wlut, q);
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, d_counter,
+                     ctx->d_wlut, q);
   HIP_TRY(hipGetLastError());
   return RT4_OK;
 }
 
-int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* rgba,
-                    int64_t row_stride_px, uint64_t* n_intersections, char* err, size_t errlen) {
-  if (!ctx || !u || !region || !rgba) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+}  // namespace
+
+extern "C" {
+
+int rt4_render_device_ex(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, void* d_frame,
+                         int32_t format, int64_t row_stride_px, unsigned long long* d_counter, void* stream,
+                         char* err, size_t errlen) {
+  if (!ctx || !u || !region || !d_frame) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  rt4_section_job job;
+  job.u = *u;
+  job.region = *region;
+  job.d_frame = d_frame;
+  job.row_stride_px = row_stride_px;
+  return launch_jobs(ctx, &job, 1, format, d_counter, stream, err, errlen);
+}
+
+int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
+                      int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err, size_t errlen) {
+  return rt4_render_device_ex(ctx, u, region, d_rgba, RT4_FRAME_RGBA32F, row_stride_px, d_counter, stream, err,
+                              errlen);
+}
+
+int rt4_render_sections_device(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, int32_t format,
+                               unsigned long long* d_counter, void* stream, char* err, size_t errlen) {
+  return launch_jobs(ctx, jobs, n_jobs, format, d_counter, stream, err, errlen);
+}
+
+int rt4_render_host_ex(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, void* frame,
+                       int32_t format, int64_t row_stride_px, uint64_t* n_intersections, char* err,
+                       size_t errlen) {
+  if (!ctx || !u || !region || !frame) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
   int st = rt4_check_render_args(u, region, row_stride_px, err, errlen);
   if (st != RT4_OK) return st;
+  const int32_t px_bytes = rt4_frame_format_bytes(format);
+  if (px_bytes == 0) return rt4_set_err(err, errlen, "unknown frame format %d", format), RT4_ERR_ARG;
   if (n_intersections) *n_intersections = 0;
   if (region->w == 0 || region->h == 0) return RT4_OK;
   HIP_TRY(hipSetDevice(ctx->device));
-  const size_t bytes = static_cast<size_t>(region->h - 1) * row_stride_px * 16 + static_cast<size_t>(region->w) * 16;
-  float* d = nullptr;
+  const size_t bytes = (static_cast<size_t>(region->h - 1) * row_stride_px + static_cast<size_t>(region->w)) * px_bytes;
+  void* d = nullptr;
   unsigned long long* dc = nullptr;
   HIP_TRY(hipMalloc(&d, bytes));
   hipError_t e = hipMalloc(&dc, sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemcpy(d, rgba, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d, frame, bytes, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemset(dc, 0, sizeof(unsigned long long));
   if (e != hipSuccess) {
     (void)hipFree(d);
@@ -937,11 +1035,11 @@ int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* r
     rt4_set_err(err, errlen, "render_host staging failed: %s", hipGetErrorString(e));
     return RT4_ERR_HIP;
   }
-  st = rt4_render_device(ctx, u, region, d, row_stride_px, dc, nullptr, err, errlen);
+  st = rt4_render_device_ex(ctx, u, region, d, format, row_stride_px, dc, nullptr, err, errlen);
   if (st == RT4_OK) {
     e = hipDeviceSynchronize();
     unsigned long long cnt = 0;
-    if (e == hipSuccess) e = hipMemcpy(rgba, d, bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(frame, d, bytes, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(&cnt, dc, sizeof(cnt), hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
       rt4_set_err(err, errlen, "render_host failed: %s", hipGetErrorString(e));
@@ -953,6 +1051,11 @@ int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* r
   (void)hipFree(d);
   (void)hipFree(dc);
   return st;
+}
+
+int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* rgba,
+                    int64_t row_stride_px, uint64_t* n_intersections, char* err, size_t errlen) {
+  return rt4_render_host_ex(ctx, u, region, rgba, RT4_FRAME_RGBA32F, row_stride_px, n_intersections, err, errlen);
 }
 
 int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_t* aux, int64_t n, char* err,

@@ -74,6 +74,8 @@ FINAL_LIGHT_SUN_SKY, FINAL_LIGHT_CONSTANT = 0, 1
 SECTION_YXZ, SECTION_YWZ, SECTION_YXW = 0, 1, 2
 FLAG_SAMPLER_LUT = 0x1
 FLAG_GENERIC_KERNEL = 0x2
+FRAME_RGBA32F, FRAME_RGBA16F, FRAME_RGBA8 = 0, 1, 2
+MAX_SECTIONS = 3
 EVAL_ACOS, EVAL_ASIN, EVAL_SIN, EVAL_COS, EVAL_VOLUME_BY_W, EVAL_W_BY_VOLUME, EVAL_HASH, EVAL_SQRT = range(8)
 
 
@@ -125,6 +127,10 @@ class Region(Structure):
     _fields_ = [("x0", c_int32), ("y0", c_int32), ("w", c_int32), ("h", c_int32), ("band_rows", c_int32), ("band_step", c_int32)]
 
 
+class SectionJob(Structure):  # rt4.h rt4_section_job
+    _fields_ = [("u", Uniforms), ("region", Region), ("d_frame", c_void_p), ("row_stride_px", c_int64)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"librt4.so not found at {LIB_PATH}: build it first (python -c 'import __graft_entry__ as g; g.build()')")
@@ -161,8 +167,18 @@ def _load():
         "rt4_debug_find_intersection": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int64] + E, c_int),
         "rt4_context_kernel_shape": ([c_void_p], c_uint32),
         "rt4_debug_verify_sqrt": ([c_void_p, POINTER(c_uint64)] + E, c_int),
+        "rt4_frame_format_bytes": ([c_int32], c_int32),
+        "rt4_render_device_ex": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int32, c_int64, c_void_p,
+                                  c_void_p] + E, c_int),
+        "rt4_render_host_ex": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int32, c_int64,
+                                POINTER(c_uint64)] + E, c_int),
+        "rt4_progressive_uniforms": ([POINTER(Uniforms), c_uint32, POINTER(Uniforms)], c_int),
+        "rt4_render_sections_device": ([c_void_p, POINTER(SectionJob), c_int32, c_int32, c_void_p, c_void_p] + E, c_int),
     }
+    tolerant = os.environ.get("RT4_AB_TOLERANT") == "1"  # tools/abtest.sh: older builds lack newer exports
     for name, (argtypes, restype) in sig.items():
+        if tolerant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)  # AttributeError if the library lacks a declared export
         fn.argtypes = argtypes
         fn.restype = restype
@@ -176,7 +192,8 @@ EXPORTED = (
     "rt4_properties_get_float rt4_properties_get_bool rt4_orientation_update rt4_section_basis "
     "rt4_uniforms_from_properties rt4_window_cells rt4_scene_load_frag rt4_scene_parse_frag rt4_scene_validate "
     "rt4_scene_builtin rt4_context_create rt4_context_set_scene rt4_context_destroy rt4_render_device rt4_render_host "
-    "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt"
+    "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt "
+    "rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -353,6 +370,21 @@ def region(w: int, h: int, x0: int = 0, y0: int = 0, band_rows: int = 0, band_st
     return Region(x0, y0, w, h, band_rows, band_step)
 
 
+def frame_format_bytes(fmt: int) -> int:
+    return lib.rt4_frame_format_bytes(fmt)
+
+
+FRAME_NUMPY = {FRAME_RGBA32F: "float32", FRAME_RGBA16F: "float16", FRAME_RGBA8: "uint8"}
+
+
+def progressive_uniforms(base: Uniforms, frame_number: int) -> Uniforms:
+    """Uniforms of progressive frame n >= 1: part = 1/n, seed_n = seed ^ n*0x9E3779B9 (rt4.h)."""
+    out = Uniforms()
+    if lib.rt4_progressive_uniforms(byref(base), frame_number, byref(out)) != 0:
+        raise RT4Error(-1, f"bad progressive frame number {frame_number}")
+    return out
+
+
 class Tracer:
     """Device context: scene on the device (+ optional sampler table) and the trace kernel."""
 
@@ -382,6 +414,37 @@ class Tracer:
         err = _errbuf()
         _check(lib.rt4_render_device(self._h, byref(u), byref(reg), c_void_p(frame_ptr), row_stride_px,
                                      c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
+
+    def render_device_ex(self, u: Uniforms, reg: Region, frame_ptr: int, fmt: int, row_stride_px: int,
+                         counter_ptr: int = 0, stream: int = 0) -> None:
+        """render_device into a device frame of any rt4_frame_format."""
+        err = _errbuf()
+        _check(lib.rt4_render_device_ex(self._h, byref(u), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
+                                        c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
+
+    def render_sections_device(self, jobs, fmt: int = FRAME_RGBA32F, counter_ptr: int = 0, stream: int = 0) -> None:
+        """One launch over up to three images: jobs = [(uniforms, region, frame_ptr, row_stride_px), ...]."""
+        arr = (SectionJob * len(jobs))()
+        for q, (u, reg, ptr, stride) in enumerate(jobs):
+            arr[q].u = u
+            arr[q].region = reg
+            arr[q].d_frame = ptr
+            arr[q].row_stride_px = stride
+        err = _errbuf()
+        _check(lib.rt4_render_sections_device(self._h, arr, len(jobs), fmt, c_void_p(counter_ptr or None),
+                                              c_void_p(stream or None), err, len(err)), err)
+
+    def render_host_ex(self, u: Uniforms, reg: Region, frame, fmt: int, row_stride_px: int | None = None) -> int:
+        """Synchronous render into a host array (h, stride, 4) of the format's dtype (FRAME_NUMPY)."""
+        import numpy as np
+
+        assert frame.dtype == np.dtype(FRAME_NUMPY[fmt]) and frame.flags["C_CONTIGUOUS"]
+        stride = row_stride_px if row_stride_px is not None else frame.shape[1]
+        n = c_uint64()
+        err = _errbuf()
+        _check(lib.rt4_render_host_ex(self._h, byref(u), byref(reg), c_void_p(frame.ctypes.data), fmt, stride,
+                                      byref(n), err, len(err)), err)
+        return n.value
 
     def render_host(self, u: Uniforms, reg: Region, frame, row_stride_px: int | None = None) -> int:
         """Synchronous render into a host float32 array of shape (h, stride, 4); returns the intersection count."""

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RT4_ABI_VERSION 1
+#define RT4_ABI_VERSION 2
 
 enum rt4_status {
   RT4_OK = 0,
@@ -248,7 +248,7 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
 int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* err, size_t errlen);
 void rt4_context_destroy(rt4_context* ctx);
 
-/* Pixel set of one launch (w <= 65535, h <= 32767). Local row i in [0,h) maps to image row
+/* Pixel set of one launch (w <= 65535, h <= 16383). Local row i in [0,h) maps to image row
  *   band_rows == 0 : y0 + i
  *   band_rows  > 0 : y0 + (i / band_rows) * band_step + (i % band_rows)
  * and local column j in [0,w) to image column x0 + j. Scene coordinates come from the full image
@@ -272,6 +272,50 @@ int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region*
  * synchronises. n_intersections (may be NULL) receives the count. */
 int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* rgba,
                     int64_t row_stride_px, uint64_t* n_intersections, char* err, size_t errlen);
+
+/* ---- frame formats, progressive accumulation, batched sections --------- */
+/* What old_frame / gl_FragColor live in. The blend mix(old, new, part) (shader.frag:524-527) is
+ * always evaluated in fp32 (one fma per channel); only the stored value differs. */
+enum rt4_frame_format {
+  RT4_FRAME_RGBA32F = 0, /* float4, 16 B/pixel (rt4_render_device) */
+  RT4_FRAME_RGBA16F = 1, /* IEEE half x4, 8 B/pixel: fp16 accumulator, stored round-to-nearest-even */
+  RT4_FRAME_RGBA8 = 2    /* unorm8 x4, 4 B/pixel: the reference's RenderTexture (windows.cpp:31), which
+                          * quantises old_frame every frame: old = u / 255.0f, stored
+                          * u = (uint8_t)(min(max(v, 0), 1) * 255.0f + 0.5f), alpha 255 */
+};
+/* Bytes per pixel of a format; 0 if unknown. */
+int32_t rt4_frame_format_bytes(int32_t format);
+
+/* rt4_render_device for any frame format: d_frame holds h rows of row_stride_px pixels of the
+ * format's size. */
+int rt4_render_device_ex(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, void* d_frame,
+                         int32_t format, int64_t row_stride_px, unsigned long long* d_counter, void* stream,
+                         char* err, size_t errlen);
+int rt4_render_host_ex(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, void* frame,
+                       int32_t format, int64_t row_stride_px, uint64_t* n_intersections, char* err,
+                       size_t errlen);
+
+/* Progressive accumulation (main.cpp:72,86-88): frame_number counts frames since the camera last
+ * moved, from 1. part = 1.0f / frame_number (frame 1 overwrites old_frame). The reference draws
+ * a fresh time-based seed every frame (main.cpp:52-54,86); this deterministic replacement is
+ * seed_n = base->seed ^ (frame_number * 0x9E3779B9). */
+int rt4_progressive_uniforms(const rt4_uniforms* base, uint32_t frame_number, rt4_uniforms* out);
+
+/* Up to three images in ONE launch: the sections of ThreeWindowGroup::drawShaderImage
+ * (three_window_group.cpp:42-46; bases from rt4_section_basis). Per job: resolution, mtr_sizes,
+ * vec_to_mtr, top_drct, right_drct, the region and the frame. seed, samples, reflections_amount,
+ * small_indent, part, light_to_color_conversion_coefficient and focus must equal jobs[0]'s (one
+ * shader, one frame; RT4_ERR_ARG otherwise). Each image equals its own rt4_render_device_ex bit for
+ * bit; the pixel queue is shared, so the sections balance each other. Region h <= 16383 here. */
+#define RT4_MAX_SECTIONS 3
+typedef struct rt4_section_job {
+  rt4_uniforms u;
+  rt4_region region;
+  void* d_frame;
+  int64_t row_stride_px;
+} rt4_section_job;
+int rt4_render_sections_device(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, int32_t format,
+                               unsigned long long* d_counter, void* stream, char* err, size_t errlen);
 
 /* ---- diagnostics (used by the parity tests; not on the render path) ------------------------- */
 enum rt4_eval_fn {

@@ -432,8 +432,73 @@ V3<F> trace(const rt4_scene_desc& s, const rt4_uniforms& u, Ray<F> ray, Rng& rng
   return acc;  // :494
 }
 
+// IEEE binary16 <-> binary32, round-to-nearest-even (what v_cvt_f16_f32 does on gfx950), denormals kept.
+inline float half_to_float(uint16_t h) {
+  const uint32_t sign = static_cast<uint32_t>(h & 0x8000u) << 16, e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+  uint32_t bits;
+  if (e == 0) {
+    if (m == 0) {
+      bits = sign;
+    } else {  // subnormal half: m * 2^-24, exact in fp32
+      float f = static_cast<float>(m) * 5.9604644775390625e-8f;
+      std::memcpy(&bits, &f, 4);
+      bits |= sign;
+    }
+  } else if (e == 31) {
+    bits = sign | 0x7F800000u | (m << 13);
+  } else {
+    bits = sign | ((e + 112u) << 23) | (m << 13);
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+inline uint16_t float_to_half(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint16_t sign = static_cast<uint16_t>((x >> 16) & 0x8000u);
+  const uint32_t ax = x & 0x7FFFFFFFu;
+  if (ax >= 0x7F800000u) return sign | (ax > 0x7F800000u ? 0x7E00u | ((ax >> 13) & 0x3FFu) : 0x7C00u);  // NaN / inf
+  if (ax >= 0x477FF000u) return sign | 0x7C00u;  // rounds to >= 65520: overflow to inf
+  if (ax < 0x38800000u) {  // below 2^-14: half subnormal (or zero), value = round(|f| * 2^24) * 2^-24
+    if (ax < 0x33000000u) return sign;  // < 2^-25: rounds to 0 (ties at exactly 2^-25 go to even = 0)
+    const uint32_t e = ax >> 23, mant = (ax & 0x7FFFFFu) | 0x800000u;
+    const uint32_t shift = 126u - e;  // 14..24
+    uint32_t q = mant >> shift;
+    const uint32_t rem = mant & ((1u << shift) - 1u), half = 1u << (shift - 1u);
+    if (rem > half || (rem == half && (q & 1u))) q++;
+    return sign | static_cast<uint16_t>(q);
+  }
+  uint32_t q = ((ax >> 13) - (112u << 10));
+  const uint32_t rem = ax & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) q++;
+  return sign | static_cast<uint16_t>(q);
+}
+
+// mix(old, new, part) in the frame format (rt4.h rt4_frame_format); the blend is fp32 in every format.
+void store_blend(void* px, int32_t fmt, const float c[3], float part) {
+  const float keep = 1.0f - part;
+  if (fmt == RT4_FRAME_RGBA16F) {
+    uint16_t* h = static_cast<uint16_t*>(px);
+    for (int q = 0; q < 3; q++) h[q] = float_to_half(std::fma(c[q], part, half_to_float(h[q]) * keep));
+    h[3] = 0x3C00u;  // 1.0
+  } else if (fmt == RT4_FRAME_RGBA8) {
+    uint8_t* b = static_cast<uint8_t*>(px);
+    for (int q = 0; q < 3; q++) {
+      const float old = static_cast<float>(b[q]) / 255.0f;
+      const float v = std::fma(c[q], part, old * keep);
+      b[q] = static_cast<uint8_t>(static_cast<uint32_t>(std::fmin(std::fmax(v, 0.0f), 1.0f) * 255.0f + 0.5f));
+    }
+    b[3] = 255;
+  } else {
+    float* f = static_cast<float*>(px);
+    for (int q = 0; q < 3; q++) f[q] = std::fma(c[q], part, f[q] * keep);
+    f[3] = 1.0f;
+  }
+}
+
 template <class F> void render_pixel(const rt4_scene_desc& s, const rt4_uniforms& u, int x, int y, float* px,
-                                     uint64_t& n_inter) {  // main :513-528
+                                     uint64_t& n_inter, int32_t fmt = RT4_FRAME_RGBA32F) {  // main :513-528
   const float sx = (static_cast<float>(x) + 0.5f) / u.resolution[0];  // :515-516 (IEEE division)
   const float sy = (static_cast<float>(y) + 0.5f) / u.resolution[1];
   Rng rng{static_cast<uint32_t>(u.seed), static_cast<uint32_t>(u.seed), fbits(sx), fbits(sy)};
@@ -452,6 +517,11 @@ template <class F> void render_pixel(const rt4_scene_desc& s, const rt4_uniforms
   const F k(u.light_to_color_conversion_coefficient);  // light_to_color :509-511
   V3<F> c = {F(1.0f) - F(1.0f) / fma_(k, light.x, F(1.0f)), F(1.0f) - F(1.0f) / fma_(k, light.y, F(1.0f)),
              F(1.0f) - F(1.0f) / fma_(k, light.z, F(1.0f))};
+  if (fmt != RT4_FRAME_RGBA32F) {  // other frame formats: the blend of store_blend, in fp32
+    const float cc[3] = {val(c.x), val(c.y), val(c.z)};
+    store_blend(px, fmt, cc, u.part);
+    return;
+  }
   const F part(u.part), keep = F(1.0f) - F(u.part);  // mix(old, new, part) :526-527
   px[0] = val(fma_(c.x, part, F(px[0]) * keep));
   px[1] = val(fma_(c.y, part, F(px[1]) * keep));
@@ -465,7 +535,8 @@ inline int region_row(const rt4_region& r, int i) {
 
 template <class F>
 void render_rows(const rt4_scene_desc& s, const rt4_uniforms& u, const rt4_region& reg, float* rgba, int64_t stride,
-                 int threads, uint64_t* n_inter, uint64_t* ops, uint32_t* pixel_counts) {
+                 int threads, uint64_t* n_inter, uint64_t* ops, uint32_t* pixel_counts, int32_t fmt = RT4_FRAME_RGBA32F) {
+  const int64_t px_bytes = fmt == RT4_FRAME_RGBA16F ? 8 : (fmt == RT4_FRAME_RGBA8 ? 4 : 16);
   std::atomic<uint64_t> total_inter{0}, total_ops{0};
   auto worker = [&](int t) {
     uint64_t my_inter = 0;
@@ -474,7 +545,9 @@ void render_rows(const rt4_scene_desc& s, const rt4_uniforms& u, const rt4_regio
       const int y = region_row(reg, i);
       for (int j = 0; j < reg.w; j++) {
         uint64_t before = my_inter;
-        render_pixel<F>(s, u, reg.x0 + j, y, rgba + 4 * (static_cast<int64_t>(i) * stride + j), my_inter);
+        render_pixel<F>(s, u, reg.x0 + j, y,
+                        reinterpret_cast<float*>(reinterpret_cast<char*>(rgba) + px_bytes * (static_cast<int64_t>(i) * stride + j)),
+                        my_inter, fmt);
         if (pixel_counts) pixel_counts[static_cast<int64_t>(i) * reg.w + j] = static_cast<uint32_t>(my_inter - before);
       }
     }
@@ -575,5 +648,20 @@ int oracle_render(const rt4_scene_desc* s, const rt4_uniforms* u, const rt4_regi
     render_rows<float>(*s, *u, *reg, rgba, row_stride_px, threads, n_intersections, nullptr, pixel_counts);
   return RT4_OK;
 }
+
+// oracle_render in a frame format (rt4.h rt4_frame_format): frame holds h rows of row_stride_px pixels.
+int oracle_render_fmt(const rt4_scene_desc* s, const rt4_uniforms* u, const rt4_region* reg, void* frame, int32_t fmt,
+                      int64_t row_stride_px, int32_t threads, uint64_t* n_intersections) {
+  if (!s || !u || !reg || !frame) return RT4_ERR_ARG;
+  if (fmt < RT4_FRAME_RGBA32F || fmt > RT4_FRAME_RGBA8) return RT4_ERR_ARG;
+  if (reg->w < 0 || reg->h < 0 || row_stride_px < reg->w) return RT4_ERR_ARG;
+  if (threads < 1) threads = 1;
+  render_rows<float>(*s, *u, *reg, static_cast<float*>(frame), row_stride_px, threads, n_intersections, nullptr, nullptr,
+                     fmt);
+  return RT4_OK;
+}
+
+uint16_t oracle_float_to_half(float f) { return float_to_half(f); }
+float oracle_half_to_float(uint16_t h) { return half_to_float(h); }
 
 }  // extern "C"

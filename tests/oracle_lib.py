@@ -86,3 +86,38 @@ def render(scene_desc, uniforms, reg, frame=None, threads=None, count_ops=False,
                              ctypes.byref(ops), counts.ctypes.data if counts is not None else None)
     assert st == 0
     return frame, n.value, ops.value, counts
+
+
+FRAME_DTYPES = {0: np.float32, 1: np.float16, 2: np.uint8}
+
+
+def render_fmt(scene_desc, uniforms, reg, fmt, frame=None, threads=None):
+    """oracle_render_fmt: renders `reg` into frame (h, w, 4) of the format's dtype (zeros if None).
+    Returns (frame, n_inter)."""
+    lib_ = lib()
+    lib_.oracle_render_fmt.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_int32,
+                                       POINTER(c_uint64)]
+    lib_.oracle_render_fmt.restype = ctypes.c_int
+    dt = FRAME_DTYPES[fmt]
+    if frame is None:
+        frame = np.zeros((reg.h, reg.w, 4), dt)
+    assert frame.dtype == dt and frame.flags["C_CONTIGUOUS"] and frame.shape[0] >= reg.h
+    n = c_uint64()
+    st = lib_.oracle_render_fmt(ctypes.addressof(scene_desc), ctypes.addressof(uniforms), ctypes.addressof(reg),
+                                frame.ctypes.data, fmt, frame.shape[1], threads or os.cpu_count() or 1, ctypes.byref(n))
+    assert st == 0
+    return frame, n.value
+
+
+def float_to_half_bits(x):
+    lib_ = lib()
+    lib_.oracle_float_to_half.argtypes = [c_float]
+    lib_.oracle_float_to_half.restype = ctypes.c_uint16
+    return np.array([lib_.oracle_float_to_half(float(v)) for v in np.asarray(x, np.float32).ravel()], np.uint16)
+
+
+def half_bits_to_float(h):
+    lib_ = lib()
+    lib_.oracle_half_to_float.argtypes = [ctypes.c_uint16]
+    lib_.oracle_half_to_float.restype = c_float
+    return np.array([lib_.oracle_half_to_float(int(v)) for v in np.asarray(h, np.uint16).ravel()], np.float32)

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol(rt4):
 def test_layout_matches_binding(rt4):
     assert ctypes.sizeof(rt4.SceneDesc) == rt4.lib.rt4_scene_desc_size()
     assert ctypes.sizeof(rt4.Uniforms) == rt4.lib.rt4_uniforms_size() == 104  # 13 uniforms, 26 words
-    assert rt4.lib.rt4_abi_version() == 1
+    assert rt4.lib.rt4_abi_version() == 2
     assert b"gfx950" in rt4.lib.rt4_build_info()
 
 

@@ -1,0 +1,123 @@
+"""GPU side of SURVEY.md 8(f) rows 1-2 against the CPU oracle, bit for bit: frame formats (fp16
+accumulator, RGBA8 as the reference's RenderTexture), progressive accumulation, and the three
+sections of ThreeWindowGroup batched into one launch. All calls go through the C ABI."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FORMATS = {"f16": 1, "rgba8": 2, "f32": 0}
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    if a.dtype == np.uint8:
+        return a == b
+    ua = a.view(np.uint16 if a.dtype == np.float16 else np.uint32)
+    ub = b.view(np.uint16 if b.dtype == np.float16 else np.uint32)
+    return (ua == ub) | (np.isnan(a) & np.isnan(b))
+
+
+@pytest.mark.parametrize("name", ["sphere", "room", "tiger_two_mirrors", "all_primitives"])
+@pytest.mark.parametrize("fmt", ["f16", "rgba8", "f32"])
+def test_progressive_formats_bitwise(rt4, oracle, name, fmt):
+    """Four progressive frames (part = 1/n, seed_n) into each frame format: GPU == oracle after every frame."""
+    f = FORMATS[fmt]
+    scene = rt4.Scene.named(name)
+    base = rt4.make_uniforms(72, 44, samples=3, reflections=4, seed=2024)
+    reg = rt4.region(72, 44)
+    dt = oracle.FRAME_DTYPES[f]
+    g = np.zeros((44, 72, 4), dt)
+    c = np.zeros((44, 72, 4), dt)
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        for n in range(1, 5):
+            u = rt4.progressive_uniforms(base, n)
+            ng = t.render_host_ex(u, reg, g, f)
+            _, nc = oracle.render_fmt(scene.desc, u, reg, f, frame=c)
+            assert ng == nc
+            eq = bits_equal(g, c)
+            assert eq.all(), f"frame {n}: {(~eq).sum()} values differ"
+    finally:
+        t.close()
+
+
+def test_fp16_accumulator_vs_fp32(rt4):
+    """BASELINE config 5 in miniature: 16 progressive frames of the all-primitive scene, fp16 accumulator
+    against fp32. Tolerance: 4e-3 absolute (half's spacing just below 1 is 2^-11 = 4.9e-4; the
+    per-frame rounding compounds over the frames)."""
+    import torch
+
+    scene = rt4.Scene.named("all_primitives")
+    base = rt4.make_uniforms(256, 160, samples=4, reflections=8, seed=12345)
+    reg = rt4.region(256, 160)
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        f32 = torch.zeros((160, 256, 4), dtype=torch.float32, device="cuda")
+        f16 = torch.zeros((160, 256, 4), dtype=torch.float16, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        for n in range(1, 17):
+            u = rt4.progressive_uniforms(base, n)
+            t.render_device_ex(u, reg, f32.data_ptr(), rt4.FRAME_RGBA32F, 256, 0, s)
+            t.render_device_ex(u, reg, f16.data_ptr(), rt4.FRAME_RGBA16F, 256, 0, s)
+        torch.cuda.synchronize()
+        d = (f16.float() - f32).abs()[..., :3]
+        assert float(d.max()) <= 4e-3, float(d.max())
+        assert float(f16[..., 3].float().min()) == 1.0
+    finally:
+        t.close()
+
+
+def section_uniforms(rt4, section, w, h, seed=77):
+    return rt4.make_uniforms(w, h, samples=3, reflections=4, seed=seed, section=section, fi=20.0, te=10.0, psi=30.0)
+
+
+@pytest.mark.parametrize("fmt", ["f32", "f16"])
+@pytest.mark.parametrize("name", ["tiger", "hypercube"])
+def test_three_sections_one_launch(rt4, oracle, name, fmt):
+    """ThreeWindowGroup::drawShaderImage (three_window_group.cpp:42-46): YXZ at the main window's
+    resolution, YWZ and YXW at the additional one's, rendered in one launch; each image equals the
+    oracle's render of that section alone, and the launch's count is the sum."""
+    import torch
+
+    f = FORMATS[fmt]
+    scene = rt4.Scene.named(name)
+    sizes = [(121, 75), (60, 37), (60, 37)]  # properties.txt:5-10 cells: 850/7 x (850/phi)/7, 600/10 x ...
+    jobs, frames, us = [], [], []
+    tdt = torch.float32 if f == 0 else torch.float16
+    for sec, (w, h) in zip((rt4.SECTION_YXZ, rt4.SECTION_YWZ, rt4.SECTION_YXW), sizes):
+        u = section_uniforms(rt4, sec, w, h)
+        fr = torch.zeros((h, w, 4), dtype=tdt, device="cuda")
+        frames.append(fr)
+        us.append(u)
+        jobs.append((u, rt4.region(w, h), fr.data_ptr(), w))
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        t.render_sections_device(jobs, f, cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        total = 0
+        for (w, h), u, fr in zip(sizes, us, frames):
+            c, nc = oracle.render_fmt(scene.desc, u, rt4.region(w, h), f)
+            total += nc
+            eq = bits_equal(fr.cpu().numpy(), c)
+            assert eq.all(), f"{(~eq).sum()} values differ"
+        assert int(cnt.item()) == total
+    finally:
+        t.close()
+
+
+def test_sections_reject_mismatched_shared_uniforms(rt4):
+    import torch
+
+    t = rt4.Tracer(device=0, scene=rt4.Scene.builtin("sphere"))
+    try:
+        fr = torch.zeros((20, 30, 4), dtype=torch.float32, device="cuda")
+        u0 = section_uniforms(rt4, rt4.SECTION_YXZ, 30, 20)
+        u1 = section_uniforms(rt4, rt4.SECTION_YWZ, 30, 20, seed=78)  # a different seed: not one frame
+        with pytest.raises(rt4.RT4Error):
+            t.render_sections_device([(u0, rt4.region(30, 20), fr.data_ptr(), 30),
+                                      (u1, rt4.region(30, 20), fr.data_ptr(), 30)])
+    finally:
+        t.close()

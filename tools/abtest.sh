@@ -34,7 +34,7 @@ elif [ "$cmd" = run ]; then
     for so in "$VDIR"/*.so; do
       name=$(basename "$so" .so)
       errf=$(mktemp)
-      out=$(RT4_LIB=$so timeout -k 10 300 python "$ROOT/bench.py" $args 2>"$errf" | tail -1)
+      out=$(RT4_AB_TOLERANT=1 RT4_LIB=$so timeout -k 10 300 python "$ROOT/bench.py" $args 2>"$errf" | tail -1)
       if [ -z "$out" ]; then echo "$name: bench failed:"; tail -5 "$errf"; rm -f "$errf"; continue; fi
       rm -f "$errf"
       python3 - "$name" "$out" <<'PY'
