@@ -7,6 +7,8 @@
 //   * the reference's five scenes as built-ins
 // Compiled with -ffp-contract=off: every fp32 expression is evaluated exactly as written.
 #include <cctype>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -314,6 +316,182 @@ int rt4_window_cells(const rt4_properties* p, const char* window_type, int32_t* 
   const unsigned height = static_cast<unsigned>(width / GOLDEN_F);  // windows.cpp:11 (unsigned member)
   *cells_w = static_cast<int32_t>(width / cell);                    // windows.cpp:25-26
   *cells_h = static_cast<int32_t>(height / cell);
+  return RT4_OK;
+}
+
+// ============================================================================ camera (controls.cpp)
+namespace {
+
+float rt4_half_to_float(uint16_t h) {  // IEEE binary16 -> binary32 (exact)
+  const uint32_t sign = static_cast<uint32_t>(h & 0x8000u) << 16, e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+  uint32_t bits;
+  if (e == 0) {
+    float f = static_cast<float>(m) * 5.9604644775390625e-8f;  // m * 2^-24 (zero or subnormal)
+    std::memcpy(&bits, &f, 4);
+    bits |= sign;
+  } else if (e == 31) {
+    bits = sign | 0x7F800000u | (m << 13);
+  } else {
+    bits = sign | ((e + 112u) << 23) | (m << 13);
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+
+void camera_normalize(rt4_camera* c) {  // SphOrientation::normalize, controls.cpp:41-50
+  normalize_angle(c->fi);
+  pull_into_range(c->te, 0, PI_F / 2);
+  if (c->constrain_psi_range)
+    pull_into_range(c->psi, c->psi_range_center, c->psi_range_radius);
+  else
+    normalize_angle(c->psi);
+}
+
+}  // namespace
+
+int rt4_camera_init(const rt4_properties* p, rt4_camera* cam, char* err, size_t errlen) {
+  if (!p || !cam) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  rt4_camera c;
+  std::memset(&c, 0, sizeof c);
+  RT4_GETF("mouse_sensitivity", c.mouse_sensitivity);  // controls.cpp:145-147
+  RT4_GETF("wheel_sensitivity", c.wheel_sensitivity);
+  RT4_GETF("movement_speed", c.movement_speed);
+  RT4_GETF("camera.focus_to_matrix_distance", c.focus_to_matrix_distance);  // main.cpp:73
+  RT4_GETF("camera.initial_position.x", c.focus[0]);                        // controls.cpp:150-156
+  RT4_GETF("camera.initial_position.y", c.focus[1]);
+  RT4_GETF("camera.initial_position.z", c.focus[2]);
+  RT4_GETF("camera.initial_position.w", c.focus[3]);
+  RT4_GETF("camera.initial_position.fi", c.fi);  // SphOrientation::init, controls.cpp:29-39
+  RT4_GETF("camera.initial_position.te", c.te);
+  RT4_GETF("camera.initial_position.psi", c.psi);
+  c.fi = deg2rad(c.fi);
+  c.te = deg2rad(c.te);
+  c.psi = deg2rad(c.psi);
+  int constrain = 0;
+  int st = rt4_properties_get_bool(p, "constrain_psi_range", &constrain, err, errlen);
+  if (st != RT4_OK) return st;
+  c.constrain_psi_range = constrain;
+  if (constrain) {
+    c.psi_range_center = c.psi;
+    normalize_angle(c.psi_range_center);
+    float deg = 0;
+    RT4_GETF("psi_range_radius", deg);
+    c.psi_range_radius = deg2rad(deg);
+  }
+  camera_normalize(&c);
+  rt4_orientation_update(c.fi, c.te, c.psi, &c.orientation);
+  c.frame_number = 1;
+  *cam = c;
+  return RT4_OK;
+}
+
+void rt4_camera_rotate(rt4_camera* cam, float d_fi, float d_te, float d_psi) {
+  if (!cam) return;
+  if (d_fi != 0.0f) { cam->fi += d_fi; normalize_angle(cam->fi); }                      // changeFi
+  if (d_te != 0.0f) { cam->te += d_te; pull_into_range(cam->te, 0, PI_F / 2); }          // changeTe
+  if (d_psi != 0.0f) {                                                                  // changePsi
+    cam->psi += d_psi;
+    if (cam->constrain_psi_range) pull_into_range(cam->psi, cam->psi_range_center, cam->psi_range_radius);
+    else normalize_angle(cam->psi);
+  }
+  rt4_orientation_update(cam->fi, cam->te, cam->psi, &cam->orientation);
+  cam->frame_number = 1;
+}
+
+int rt4_camera_mouse_move(rt4_camera* cam, int32_t dx, int32_t dy, uint32_t max_offset) {
+  if (!cam) return 0;
+  if (static_cast<uint32_t>(std::abs(dx)) > max_offset || static_cast<uint32_t>(std::abs(dy)) > max_offset)
+    return 1;  // centerMouseCursor() only (controls.cpp:185-186)
+  if (dx == 0 && dy == 0) return 0;
+  rt4_camera_rotate(cam, static_cast<float>(dx) * cam->mouse_sensitivity, static_cast<float>(dy) * cam->mouse_sensitivity,
+                    0.0f);
+  return 0;
+}
+
+void rt4_camera_wheel(rt4_camera* cam, float delta) {
+  if (!cam) return;
+  rt4_camera_rotate(cam, 0.0f, 0.0f, delta * cam->wheel_sensitivity);
+  cam->frame_number = 1;  // also when a constrained psi did not change (controls.cpp:199)
+}
+
+void rt4_camera_move(rt4_camera* cam, uint32_t keys, float seconds) {  // controls.cpp:118-134
+  if (!cam) return;
+  const rt4_orientation& o = cam->orientation;
+  float d[4] = {0, 0, 0, 0};
+  auto add = [&](const float* v, float sgn) {  // sum(drct, v) / dif(drct, v) = sum(drct, mulVN(v, -1))
+    for (int k = 0; k < 4; k++) d[k] = d[k] + v[k] * sgn;
+  };
+  if (keys & RT4_KEY_FORWARD) add(o.horizontal_forward, 1.0f);
+  if (keys & RT4_KEY_BACK) add(o.horizontal_forward, -1.0f);
+  if (keys & RT4_KEY_UP) add(o.vertical_top, 1.0f);
+  if (keys & RT4_KEY_DOWN) add(o.vertical_top, -1.0f);
+  if (keys & RT4_KEY_RIGHT) add(o.horizontal_right, 1.0f);
+  if (keys & RT4_KEY_LEFT) add(o.horizontal_right, -1.0f);
+  if (keys & RT4_KEY_W_POS) add(o.w_drct, 1.0f);
+  if (keys & RT4_KEY_W_NEG) add(o.w_drct, -1.0f);
+  const float len = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]);  // mod(), math.cpp:12-13
+  if (len > 0) {
+    const float k = seconds * cam->movement_speed / len;
+    for (int q = 0; q < 4; q++) cam->focus[q] = cam->focus[q] + d[q] * k;
+    cam->frame_number = 1;
+  }
+}
+
+int rt4_camera_frame_uniforms(rt4_camera* cam, const rt4_uniforms* base, int section, int32_t seed,
+                              rt4_uniforms* out) {
+  if (!cam || !base || !out || cam->frame_number == 0) return RT4_ERR_ARG;
+  rt4_uniforms u = *base;
+  u.seed = seed;                                                 // main.cpp:86
+  u.part = 1.0f / static_cast<float>(cam->frame_number);         // main.cpp:87
+  std::memcpy(u.focus, cam->focus, sizeof u.focus);              // main.cpp:89
+  for (int k = 0; k < 4; k++) u.vec_to_mtr[k] = cam->orientation.forward[k] * cam->focus_to_matrix_distance;  // :90
+  if (rt4_section_basis(&cam->orientation, section, u.top_drct, u.right_drct) != RT4_OK) return RT4_ERR_ARG;
+  cam->frame_number++;                                           // frameNumber++ (main.cpp:88)
+  *out = u;
+  return RT4_OK;
+}
+
+// ============================================================================ image output
+int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                  char* err, size_t errlen) {
+  if (!path || !frame || w <= 0 || h <= 0 || row_stride_px < w)
+    return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
+  const int32_t px_bytes = rt4_frame_format_bytes(format);
+  if (px_bytes == 0) return rt4_set_err(err, errlen, "unknown frame format %d", format), RT4_ERR_ARG;
+  std::FILE* f = std::fopen(path, "wb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s for writing", path), RT4_ERR_IO;
+  std::fprintf(f, "P6\n%d %d\n255\n", w, h);
+  std::vector<unsigned char> row(static_cast<size_t>(w) * 3);
+  auto q8 = [](float v) {  // the RGBA8 rule of rt4_frame_format
+    return static_cast<unsigned char>(static_cast<uint32_t>(std::fmin(std::fmax(v, 0.0f), 1.0f) * 255.0f + 0.5f));
+  };
+  for (int32_t i = 0; i < h; i++) {
+    const unsigned char* base = static_cast<const unsigned char*>(frame) + static_cast<size_t>(i) * row_stride_px * px_bytes;
+    for (int32_t j = 0; j < w; j++) {
+      const unsigned char* px = base + static_cast<size_t>(j) * px_bytes;
+      for (int c = 0; c < 3; c++) {
+        unsigned char v;
+        if (format == RT4_FRAME_RGBA8) {
+          v = px[c];
+        } else if (format == RT4_FRAME_RGBA16F) {
+          uint16_t hb;
+          std::memcpy(&hb, px + 2 * c, 2);
+          v = q8(rt4_half_to_float(hb));
+        } else {
+          float fv;
+          std::memcpy(&fv, px + 4 * c, 4);
+          v = q8(fv);
+        }
+        row[static_cast<size_t>(j) * 3 + c] = v;
+      }
+    }
+    if (std::fwrite(row.data(), 1, row.size(), f) != row.size()) {
+      std::fclose(f);
+      return rt4_set_err(err, errlen, "write failed: %s", path), RT4_ERR_IO;
+    }
+  }
+  if (std::fclose(f) != 0) return rt4_set_err(err, errlen, "close failed: %s", path), RT4_ERR_IO;
   return RT4_OK;
 }
 

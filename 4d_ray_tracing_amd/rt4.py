@@ -75,6 +75,7 @@ SECTION_YXZ, SECTION_YWZ, SECTION_YXW = 0, 1, 2
 FLAG_SAMPLER_LUT = 0x1
 FLAG_GENERIC_KERNEL = 0x2
 FRAME_RGBA32F, FRAME_RGBA16F, FRAME_RGBA8 = 0, 1, 2
+KEY_FORWARD, KEY_BACK, KEY_RIGHT, KEY_LEFT, KEY_UP, KEY_DOWN, KEY_W_POS, KEY_W_NEG = (1 << i for i in range(8))
 MAX_SECTIONS = 3
 EVAL_ACOS, EVAL_ASIN, EVAL_SIN, EVAL_COS, EVAL_VOLUME_BY_W, EVAL_W_BY_VOLUME, EVAL_HASH, EVAL_SQRT = range(8)
 
@@ -123,6 +124,13 @@ class OrientationStruct(Structure):  # struct Orientation, inc/controls.h:9-14
     _fields_ = [(n, F4) for n in ("forward", "top", "right", "w_drct", "horizontal_forward", "horizontal_right", "vertical_top")]
 
 
+class CameraStruct(Structure):  # rt4.h rt4_camera (SphOrientation + controls.cpp state)
+    _fields_ = [("fi", c_float), ("te", c_float), ("psi", c_float), ("psi_range_center", c_float),
+                ("psi_range_radius", c_float), ("constrain_psi_range", c_int32), ("mouse_sensitivity", c_float),
+                ("wheel_sensitivity", c_float), ("movement_speed", c_float), ("focus_to_matrix_distance", c_float),
+                ("focus", F4), ("frame_number", c_uint32), ("orientation", OrientationStruct)]
+
+
 class Region(Structure):
     _fields_ = [("x0", c_int32), ("y0", c_int32), ("w", c_int32), ("h", c_int32), ("band_rows", c_int32), ("band_step", c_int32)]
 
@@ -168,6 +176,13 @@ def _load():
         "rt4_context_kernel_shape": ([c_void_p], c_uint32),
         "rt4_debug_verify_sqrt": ([c_void_p, POINTER(c_uint64)] + E, c_int),
         "rt4_frame_format_bytes": ([c_int32], c_int32),
+        "rt4_camera_init": ([c_void_p, POINTER(CameraStruct)] + E, c_int),
+        "rt4_camera_rotate": ([POINTER(CameraStruct), c_float, c_float, c_float], None),
+        "rt4_camera_mouse_move": ([POINTER(CameraStruct), c_int32, c_int32, c_uint32], c_int),
+        "rt4_camera_wheel": ([POINTER(CameraStruct), c_float], None),
+        "rt4_camera_move": ([POINTER(CameraStruct), c_uint32, c_float], None),
+        "rt4_camera_frame_uniforms": ([POINTER(CameraStruct), POINTER(Uniforms), c_int, c_int32, POINTER(Uniforms)], c_int),
+        "rt4_write_ppm": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64] + E, c_int),
         "rt4_render_device_ex": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int32, c_int64, c_void_p,
                                   c_void_p] + E, c_int),
         "rt4_render_host_ex": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int32, c_int64,
@@ -193,7 +208,8 @@ EXPORTED = (
     "rt4_uniforms_from_properties rt4_window_cells rt4_scene_load_frag rt4_scene_parse_frag rt4_scene_validate "
     "rt4_scene_builtin rt4_context_create rt4_context_set_scene rt4_context_destroy rt4_render_device rt4_render_host "
     "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt "
-    "rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device"
+    "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
+    "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -368,6 +384,49 @@ class Scene:
 
 def region(w: int, h: int, x0: int = 0, y0: int = 0, band_rows: int = 0, band_step: int = 0) -> Region:
     return Region(x0, y0, w, h, band_rows, band_step)
+
+
+class Camera:
+    """The reference's camera controller (src/controls.cpp) over rt4_camera: mouse/wheel rotation,
+    WASD/Space/Shift/E/Q motion and per-frame uniforms (main.cpp:86-91)."""
+
+    def __init__(self, props: "Properties"):
+        self.s = CameraStruct()
+        err = _errbuf()
+        _check(lib.rt4_camera_init(props._h, byref(self.s), err, len(err)), err)
+
+    def rotate(self, d_fi=0.0, d_te=0.0, d_psi=0.0):
+        lib.rt4_camera_rotate(byref(self.s), d_fi, d_te, d_psi)
+
+    def mouse_move(self, dx: int, dy: int, max_offset: int) -> bool:
+        """True when the move only re-centres the cursor (out of the allowed offset)."""
+        return bool(lib.rt4_camera_mouse_move(byref(self.s), dx, dy, max_offset))
+
+    def wheel(self, delta: float):
+        lib.rt4_camera_wheel(byref(self.s), delta)
+
+    def move(self, keys: int, seconds: float):
+        lib.rt4_camera_move(byref(self.s), keys, seconds)
+
+    def frame_uniforms(self, base: Uniforms, section: int = SECTION_YXZ, seed: int = 0) -> Uniforms:
+        out = Uniforms()
+        seed = ctypes.c_int32(seed & 0xFFFFFFFF).value
+        if lib.rt4_camera_frame_uniforms(byref(self.s), byref(base), section, seed, byref(out)) != 0:
+            raise RT4Error(-1, "rt4_camera_frame_uniforms failed")
+        return out
+
+
+def write_ppm(path: str, frame, fmt: int | None = None) -> None:
+    """Binary PPM of an (h, w, 4) frame (float32 / float16 / uint8), rows top first (rt4_write_ppm)."""
+    import numpy as np
+
+    frame = np.ascontiguousarray(frame)
+    if fmt is None:
+        fmt = {np.dtype("float32"): FRAME_RGBA32F, np.dtype("float16"): FRAME_RGBA16F,
+               np.dtype("uint8"): FRAME_RGBA8}[frame.dtype]
+    h, w = frame.shape[:2]
+    err = _errbuf()
+    _check(lib.rt4_write_ppm(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, err, len(err)), err)
 
 
 def frame_format_bytes(fmt: int) -> int:

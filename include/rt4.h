@@ -223,6 +223,58 @@ int rt4_uniforms_from_properties(const rt4_properties* p, int32_t cells_w, int32
 int rt4_window_cells(const rt4_properties* p, const char* window_type, int32_t* cells_w, int32_t* cells_h,
                      char* err, size_t errlen);
 
+/* ---- camera model: SphOrientation, mouse / wheel / WASD-EQ motion (src/controls.cpp) ---------- */
+typedef struct rt4_camera {
+  float fi, te, psi;                       /* radians, normalised (SphOrientation, controls.cpp:25-54) */
+  float psi_range_center, psi_range_radius;
+  int32_t constrain_psi_range;
+  float mouse_sensitivity, wheel_sensitivity, movement_speed; /* controls.cpp:144-147 */
+  float focus_to_matrix_distance;          /* main.cpp:73 */
+  float focus[4];                          /* controls.cpp:150-156 */
+  uint32_t frame_number;                   /* frames since the camera last changed, from 1 (main.cpp:72) */
+  rt4_orientation orientation;             /* Orientation::update() of (fi, te, psi) */
+} rt4_camera;
+
+/* Movement keys held during a frame (controls.cpp:98-113). */
+enum rt4_move_key {
+  RT4_KEY_FORWARD = 1,  /* W      horizontal_forward */
+  RT4_KEY_BACK = 2,     /* S     -horizontal_forward */
+  RT4_KEY_RIGHT = 4,    /* D      horizontal_right   */
+  RT4_KEY_LEFT = 8,     /* A     -horizontal_right   */
+  RT4_KEY_UP = 16,      /* Space  vertical_top       */
+  RT4_KEY_DOWN = 32,    /* LShift -vertical_top      */
+  RT4_KEY_W_POS = 64,   /* E      w_drct             */
+  RT4_KEY_W_NEG = 128   /* Q     -w_drct             */
+};
+
+/* initControls + SphOrientation::init (controls.cpp:140-159, :29-39): angles from degrees, psi range,
+ * sensitivities, speed, focus; frame_number = 1. */
+int rt4_camera_init(const rt4_properties* p, rt4_camera* cam, char* err, size_t errlen);
+/* changeFi / changeTe / changePsi (each re-normalises) + Orientation::update + frame_number = 1
+ * (controls.cpp:51-53, :186-198). */
+void rt4_camera_rotate(rt4_camera* cam, float d_fi, float d_te, float d_psi);
+/* Event::MouseMoved with the cursor (dx, dy) from the window centre, dy up (controls.cpp:181-193):
+ * returns 1 and changes nothing when |dx| or |dy| exceeds max_offset (the cursor is re-centred),
+ * 0 after rotating by (dx, dy) * mouse_sensitivity (a zero move changes nothing). */
+int rt4_camera_mouse_move(rt4_camera* cam, int32_t dx, int32_t dy, uint32_t max_offset);
+/* Event::MouseWheelScrolled: psi += delta * wheel_sensitivity (controls.cpp:196-201). */
+void rt4_camera_wheel(rt4_camera* cam, float delta);
+/* move(seconds) (controls.cpp:118-134): focus += drct * (seconds * movement_speed / |drct|) for the
+ * sum drct of the held keys' directions; frame_number = 1 when it moved. */
+void rt4_camera_move(rt4_camera* cam, uint32_t keys, float seconds);
+/* Uniforms of the next frame (main.cpp:86-91, windows.cpp:41-44): base supplies samples,
+ * reflections_amount, small_indent, k, mtr_sizes and resolution; then seed, part = 1/frame_number,
+ * focus, vec_to_mtr = forward * focus_to_matrix_distance and top/right of `section`. Advances
+ * frame_number (frameNumber++). */
+int rt4_camera_frame_uniforms(rt4_camera* cam, const rt4_uniforms* base, int section, int32_t seed,
+                              rt4_uniforms* out);
+
+/* ---- image output (presentation; windows.cpp:24-53 shows frames in SFML windows instead) ------ */
+/* Binary PPM (P6) of an RGBA frame in any rt4_frame_format, rows top first, alpha dropped; float
+ * channels are clamped to [0, 1] and mapped with the RGBA8 rule u = (uint8)(v * 255 + 0.5). */
+int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                  char* err, size_t errlen);
+
 /* ---- scenes ------------------------------------------------------------------------------- */
 /* Accepts a scene snippet (scenes/<name>.frag) or a whole shader.frag; UTF-8 paths. */
 int rt4_scene_load_frag(const char* path, rt4_scene_desc* out, char* err, size_t errlen);
