@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from ctypes import POINTER, Structure, byref, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -448,6 +449,14 @@ class Tracer:
     """Device context: scene on the device (+ optional sampler table) and the trace kernel."""
 
     def __init__(self, device: int = 0, flags: int = 0, scene: Scene | None = None):
+        # librt4.so links the system HIP runtime; PyTorch-ROCm brings its own copy. In one process the
+        # torch runtime must initialise first (torch.cuda reports no GPU when it comes second).
+        torch = sys.modules.get("torch")
+        if torch is not None and hasattr(torch, "cuda") and not torch.cuda.is_initialized():
+            try:
+                torch.cuda.init()
+            except Exception:  # no GPU for torch: librt4.so reports its own error below
+                pass
         h = c_void_p()
         err = _errbuf()
         _check(lib.rt4_context_create(device, flags, byref(h), err, len(err)), err)

@@ -17,7 +17,14 @@ def pytest_configure(config):
 
 
 @pytest.fixture(scope="session")
-def rt4():
+def rt4(request):
+    # GPU sessions: bring up PyTorch's HIP runtime before librt4.so's (rt4.Tracer does the same when
+    # torch is already imported); torch.cuda finds no GPU if it initialises second in the process.
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
     return importlib.import_module("4d_ray_tracing_amd")
 
 

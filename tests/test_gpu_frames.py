@@ -121,3 +121,60 @@ def test_sections_reject_mismatched_shared_uniforms(rt4):
                                       (u1, rt4.region(30, 20), fr.data_ptr(), 30)])
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("keys,fmt", [("", "f32"), ("WE", "rgba8")])
+def test_cpp_host_program_matches_python_driver(rt4, tmp_path, keys, fmt):
+    """lib/rt4_render (the C++ host over the C ABI: main.cpp's frame loop offscreen, three sections,
+    progressive frames, optional WASD/EQ motion between frames) writes the same PPMs as the same loop
+    driven from Python through the same ABI."""
+    import os
+    import subprocess
+
+    import torch
+
+    props_text = open(os.path.join(os.path.dirname(rt4.LIB_PATH), "..", "..", "properties.txt")).read()
+    props_text = (props_text.replace("window.main.width = 850", "window.main.width = 140")
+                  .replace("window.main.cell_size = 7", "window.main.cell_size = 2")
+                  .replace("window.additional.width = 600", "window.additional.width = 100")
+                  .replace("window.additional.cell_size = 10", "window.additional.cell_size = 4")
+                  .replace("ray_tracing.samples = 100", "ray_tracing.samples = 2")
+                  .replace("ray_tracing.reflections_amount = 4", "ray_tracing.reflections_amount = 3"))
+    pfile = tmp_path / "properties.txt"
+    pfile.write_text(props_text)
+    exe = os.path.join(os.path.dirname(rt4.LIB_PATH), "rt4_render")
+    cmd = [exe, "-p", str(pfile), "-s", "tiger", "-n", "3", "-3", "-f", fmt, "--seed", "4242", "-o", str(tmp_path / "cpp")]
+    if keys:
+        cmd += ["--keys", keys, "--move-seconds", "0.05"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+
+    f = FORMATS[fmt]
+    props = rt4.Properties(text=props_text)
+    cam = rt4.Camera(props)
+    cells = [rt4.window_cells(props, "main"), rt4.window_cells(props, "additional"), rt4.window_cells(props, "additional")]
+    secs = [rt4.SECTION_YXZ, rt4.SECTION_YWZ, rt4.SECTION_YXW]
+    bases = [rt4.uniforms_from_properties(props, w, h, s) for (w, h), s in zip(cells, secs)]
+    tdt = {0: torch.float32, 1: torch.float16, 2: torch.uint8}[f]
+    frames = [torch.zeros((h, w, 4), dtype=tdt, device="cuda") for (w, h) in cells]
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=rt4.Scene.builtin("tiger"))
+    keymask = sum({"W": rt4.KEY_FORWARD, "E": rt4.KEY_W_POS}[c] for c in keys)
+    try:
+        for n in range(1, 4):
+            seed = 4242 ^ ((n * 0x9E3779B9) & 0xFFFFFFFF)
+            fn = cam.s.frame_number
+            jobs = []
+            for q in range(3):
+                cam.s.frame_number = fn
+                u = cam.frame_uniforms(bases[q], secs[q], seed)
+                jobs.append((u, rt4.region(*cells[q]), frames[q].data_ptr(), cells[q][0]))
+            t.render_sections_device(jobs, f)
+            if keymask:
+                cam.move(keymask, 0.05)
+        torch.cuda.synchronize()
+    finally:
+        t.close()
+    for q, name in enumerate(("yxz", "ywz", "yxw")):
+        ref = tmp_path / f"py_{name}.ppm"
+        rt4.write_ppm(str(ref), frames[q].cpu().numpy(), f)
+        assert (tmp_path / f"cpp_{name}.ppm").read_bytes() == ref.read_bytes(), name
