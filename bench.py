@@ -4,11 +4,13 @@
 Workload (BASELINE.json configs[1]): the sphere+plane+sun scene
 (scenes/Шар, плоскость и светилник.frag), 1920x1080 pixels per GPU, 16 samples, 8 reflections,
 seed 12345, default camera, old_frame = 0, part = 1. One "step" = one frame = one launch of the trace
-kernel over the rank's pixels (+ the RCCL gather to rank 0 when N > 1). The unit is one
-find_intersection() call (shader.frag:475), counted on the device by the kernel itself.
+kernel over the rank's pixels. The unit is one find_intersection() call (shader.frag:475), counted
+on the device by the kernel itself.
 
 Multi-GPU (torchrun): weak scaling — each rank renders 1920x1080 pixels of a 1920x(1080*N) frame,
-dealt in 8-row bands round-robin (4d_ray_tracing_amd/shard.py), then one gather to rank 0.
+dealt in 8-row bands round-robin (4d_ray_tracing_amd/shard.py). The frame is assembled on rank 0 by
+ONE RCCL gather after the K frames, inside the timed region (accumulate locally,
+gather once); --gather every gathers after every frame instead.
 
 Prints ONE JSON line on rank 0 with `roofline` (fp32 VALU: oracle-counted fp32 ops per unit x units
 per launch / average kernel time, vs the 157.3 TFLOP/s gfx950 vector peak) and `cpu_baseline`
@@ -42,6 +44,9 @@ def parse_args():
     p.add_argument("--no-lut", action="store_true", help="disable the w_by_volume table (inline Newton loop)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--format", choices=["f32", "f16", "rgba8"], default="f32", help="frame format (rt4_frame_format)")
+    p.add_argument("--gather", choices=["final", "every"], default="final",
+                   help="N > 1: one RCCL gather after the timed frames (default) or one per frame")
     return p.parse_args()
 
 
@@ -98,7 +103,9 @@ def pmc_traffic(config):
         return None, None
     d = json.load(open(path))
     keys = ("width", "height_per_gpu", "spp", "bounces", "seed", "sampler_lut")
-    if any(d.get("config", {}).get(k) != config[k] for k in keys):
+    pc = dict(d.get("config", {}))
+    pc.setdefault("frame_format", "f32")  # profiles before frame formats existed were float4
+    if any(pc.get(k) != config[k] for k in keys + ("frame_format",)):
         return None, None
     return d["derived"].get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
@@ -125,13 +132,18 @@ def main():
     u = rt4.make_uniforms(plan.width, plan.height, samples=args.spp, reflections=args.bounces, seed=args.seed)
     reg = rt4.region(**plan.region_args(rank))
 
-    frame = torch.zeros((plan.rows_per_rank, plan.width, 4), dtype=torch.float32, device=dev)
+    fmt = {"f32": rt4.FRAME_RGBA32F, "f16": rt4.FRAME_RGBA16F, "rgba8": rt4.FRAME_RGBA8}[args.format]
+    tdt = {"f32": torch.float32, "f16": torch.float16, "rgba8": torch.uint8}[args.format]
+    frame = torch.zeros((plan.rows_per_rank, plan.width, 4), dtype=tdt, device=dev)
     counter = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
+    def render():
+        tracer.render_device_ex(u, reg, frame.data_ptr(), fmt, plan.width, counter.data_ptr(), sptr)
+
     def step():
-        tracer.render_device(u, reg, frame.data_ptr(), plan.width, counter.data_ptr(), sptr)
+        render()
         if world > 1:
             shard.gather_frame(frame, plan, rank)
 
@@ -147,16 +159,23 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         k_start[i].record(stream)
-        tracer.render_device(u, reg, frame.data_ptr(), plan.width, counter.data_ptr(), sptr)
+        render()
         k_end[i].record(stream)
-        if world > 1:
+        if world > 1 and args.gather == "every":
             shard.gather_frame(frame, plan, rank)
+    g0 = torch.cuda.Event(enable_timing=True)
+    g1 = torch.cuda.Event(enable_timing=True)
+    g0.record(stream)
+    if world > 1 and args.gather == "final":
+        shard.gather_frame(frame, plan, rank)  # the frame assembled on rank 0
+    g1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / args.steps
 
+    gather_ms = g0.elapsed_time(g1)
     n_local = int(counter.item())
     stats = torch.tensor([elapsed, float(n_local), kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -194,8 +213,10 @@ def main():
                 "scene": args.scene, "width": plan.width, "height_per_gpu": plan.rows_per_rank,
                 "spp": args.spp, "bounces": args.bounces, "seed": args.seed,
                 "sampler_lut": not args.no_lut,
-                "parallelism": f"pixel-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"pixel-bands x{world}" + (f" + RCCL gather ({args.gather})" if world > 1 else ""),
+                "frame_format": args.format,
             },
+            "gather_ms": gather_ms if world > 1 else 0.0,
             "intersections_per_step": n_total / args.steps,
             "nominal_bound_per_step": plan.width * plan.height * args.spp * (args.bounces + 1),
             "kernel_ms": kernel_ms,
