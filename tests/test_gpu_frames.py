@@ -178,3 +178,28 @@ def test_cpp_host_program_matches_python_driver(rt4, tmp_path, keys, fmt):
         ref = tmp_path / f"py_{name}.ppm"
         rt4.write_ppm(str(ref), frames[q].cpu().numpy(), f)
         assert (tmp_path / f"cpp_{name}.ppm").read_bytes() == ref.read_bytes(), name
+
+
+def test_sections_argument_checks_and_empty_job(rt4, oracle):
+    import torch
+
+    scene = rt4.Scene.builtin("sphere")
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        fr = torch.zeros((20, 30, 4), dtype=torch.float32, device="cuda")
+        u = section_uniforms(rt4, rt4.SECTION_YXZ, 30, 20)
+        job = (u, rt4.region(30, 20), fr.data_ptr(), 30)
+        with pytest.raises(rt4.RT4Error):
+            t.render_sections_device([job] * 4)  # more than RT4_MAX_SECTIONS
+        with pytest.raises(rt4.RT4Error):
+            t.render_sections_device([job], fmt=9)  # unknown frame format
+        with pytest.raises(rt4.RT4Error):
+            t.render_sections_device([(u, rt4.region(30, 16384), fr.data_ptr(), 30)])  # h > 16383
+        # an empty section next to a real one: the real one renders as if alone
+        u2 = section_uniforms(rt4, rt4.SECTION_YWZ, 30, 20)
+        t.render_sections_device([(u2, rt4.region(0, 0), 0, 0), job])
+        torch.cuda.synchronize()
+        c, _ = oracle.render_fmt(scene.desc, u, rt4.region(30, 20), 0)
+        assert bits_equal(fr.cpu().numpy(), c).all()
+    finally:
+        t.close()

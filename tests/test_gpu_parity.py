@@ -108,6 +108,27 @@ def test_scene_runs_exact_count_kernel(rt4, name):
         t.close()
 
 
+def test_untested_objects_keep_primitive_ids(rt4, oracle):
+    """A scene that defines a union the group list never tests: the flat primitive table still holds
+    its two entries, so the exact-count kernel (compile-time table bases) must not be chosen; the
+    runtime-count kernel renders it bit-exactly."""
+    base = rt4.Scene.builtin("hypercube")
+    d = rt4.SceneDesc.from_buffer_copy(bytes(base.desc))
+    d.n_unions = 1
+    d.unions[0] = rt4.Scene.builtin("cylinder4d").desc.unions[0]
+    scene = rt4.Scene(d)
+    t = rt4.Tracer(device=0, scene=scene)
+    try:
+        k = t.kernel_shape
+    finally:
+        t.close()
+    assert k == (1 | 16)  # spaces + hypercube, counts read at run time
+    u = rt4.make_uniforms(64, 40, samples=3, reflections=4, seed=5)
+    fg, ng, fc, nc = render_both(rt4, oracle, scene, u, rt4.region(64, 40), flags=rt4.FLAG_SAMPLER_LUT)
+    assert ng == nc
+    assert_bits(fg, fc, "hypercube + untested union")
+
+
 # ------------------------------------------------------------------------------- intersections
 def random_rays(n, seed):
     rng = np.random.default_rng(seed)
