@@ -56,6 +56,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e.x; }
 using WEntry = float;
 __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #endif
+#ifndef RT4_TILE_ORDER
+#define RT4_TILE_ORDER 0  // order the queue hands out a job's 8x8 tiles: 0 row-major from the top, 1 reversed
+#endif
 #ifndef RT4_SKY_PRETEST
 #define RT4_SKY_PRETEST 1
 #endif
@@ -86,6 +89,17 @@ constexpr int QUEUE_SLOTS = 64;     // rotating per-launch queue words (see rt4_
 #else
 #define RT4_STAMP(var) (void)0
 #define RT4_ACC(slot, t0) (void)0
+#endif
+// Diagnostic build only (-DRT4_LANESTATS, never shipped): per phase, wave executions and active lanes
+// (popcount of exec) into counter[16 + 2p], counter[17 + 2p] (tools/lanestats.py).
+#ifdef RT4_LANESTATS
+#define RT4_LS(p)                                                          \
+  do {                                                                     \
+    ls[2 * (p)] += 1;                                                      \
+    ls[2 * (p) + 1] += __popcll(__builtin_amdgcn_read_exec());             \
+  } while (0)
+#else
+#define RT4_LS(p) (void)0
 #endif
 
 // find_intersection front-ends: the generic group loop returns a full Hit; the specialised path
@@ -305,6 +319,9 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   int s = 0, b = 0;
   uint32_t n_inter = 0;
 
+#ifdef RT4_LANESTATS
+  unsigned long long ls[20] = {};
+#endif
 #ifdef RT4_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;
   RT4_STAMP(t_loop0);
@@ -322,6 +339,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     if (!exhausted) {
       const unsigned long long idle = __ballot(!active);
       if (static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN) {
+        RT4_LS(8);
         if (pending) {
           flush_pixel();
           pending = false;
@@ -349,7 +367,11 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
           const JobArgs& J = a.jobs[job];
           if (!active && rank >= got && rank < got + n) {
             const unsigned idx = b_next + (rank - got);
-            const unsigned tile = (idx >> 6) - J.tile_base, l = idx & 63u;
+            unsigned tile = (idx >> 6) - J.tile_base;
+            const unsigned l = idx & 63u;
+#if RT4_TILE_ORDER == 1  // bottom-up: the last tiles handed out are the top rows
+            tile = J.tiles_x * ((static_cast<unsigned>(J.reg.h) + 7u) >> 3) - 1u - tile;
+#endif
             const int jj = static_cast<int>((tile % J.tiles_x) * 8u + (l & 7u));
             const int ii = static_cast<int>((tile / J.tiles_x) * 8u + (l >> 3));
             if (jj < J.reg.w && ii < J.reg.h) {
@@ -379,11 +401,16 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
       }
     }
     RT4_ACC(0, t_ph);
+#ifdef RT4_LANESTATS
+    ls[0] += 1;
+    ls[1] += __popcll(__ballot(active));
+#endif
     if (!__any(active)) {
       if (exhausted) break;
       continue;
     }
     if (active) {
+      RT4_LS(1);
       RT4_STAMP(t_ph);
       WEntry w_pre{};  // sampler-table entry for this iteration's diffuse bounce (LUT path)
       const typename Finder<K>::R c = Finder<K>::find(S, X, P, ray);  // :475
@@ -391,12 +418,14 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
       ++n_inter;
       bool end;
       if (!c.hit) {  // :477-479
+        RT4_LS(3);
         RT4_STAMP(t_ph);
         const V3 fl = final_light(S, X, ray.drct);
         RT4_ACC(2, t_ph);
         acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
         end = true;
       } else {
+        RT4_LS(4);
 #if RT4_LUT_PREFETCH == 2
 #ifdef RT4_ABL_NOLUT  // ablation only (wrong images): the index arithmetic without the table gather
         if (LUT) w_pre = WEntry{static_cast<float>(next_diffuse_w_index(rng)) * 2.3841858e-7f - 1.0f};
@@ -415,9 +444,11 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
         ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                  // :485
         if (!(rand_(rng) > refl)) {  // :488 rand_outcome -> reflect
+          RT4_LS(5);
           const float dn = dot(h.norm, ray.drct);
           ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
         } else {  // :491 redirect(rand_drct(), norm)
+          RT4_LS(6);
           RT4_STAMP(t_ph);
           const V4 v = rand_drct<LUT>(rng, wlut, w_pre);
           RT4_ACC(4, t_ph);
@@ -428,6 +459,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         end = b > R;
       }
       if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
+        RT4_LS(7);
         const float4 lp = cold[256];
         cold[256] = make_float4(lp.x + acc.x, lp.y + acc.y, lp.z + acc.z, lp.w);
         const float4 c0 = cold[0];
@@ -444,6 +476,10 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     }
   }
   if (pending) flush_pixel();
+#ifdef RT4_LANESTATS
+  if (counter && lane == 0)
+    for (int q = 0; q < 20; q++) atomicAdd(counter + 16 + q, ls[q]);
+#endif
 #ifdef RT4_STAMPS
   RT4_ACC(5, t_loop0);
   if (counter && lane == 0)
