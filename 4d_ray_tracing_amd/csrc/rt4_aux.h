@@ -62,6 +62,27 @@ struct alignas(32) SphereCull {
   float pad[2];
 };
 
+// Bounding hypersphere of a tiger / cylinders union (rt4_fast.h far_from): every point the exact test
+// can report as a hit lies on one cylinder (distance r from its axes plane, up to ~1e-5 relative) and
+// passes the other cylinder's axes-distance filter (d^2 <= gt). When the two axes planes are
+// orthogonal complements through the same point (init_tiger / the reference's unions), those two
+// distances are the point's coordinates in the two planes, so |q - c|^2 <= r^2 + gt = R^2. A ray whose
+// LINE keeps its distance^2 to c above R2m = R^2 (1 + 1e-3) (+ 4e-6 |p - c|^2 for the fp32
+// evaluation) cannot produce a real hit. The one other way these tests report a hit is a NaN
+// distance: sqrt(r^2 + len_po^2 - 2 r len_po cos) of a slightly negative rounding of (len_po - r)^2,
+// i.e. a ray starting on (within ~5e-4 r of) one of the infinite cylinders, anywhere; the NaN then
+// passes the filters (the reference's comparisons are false on NaN). So the skip also requires the
+// origin's squared distance to each axes plane to stay out of [0.99 r^2, 1.01 r^2] for the radii of
+// that plane's cylinders (band[]). Then the skipped test's result is exactly "no hit".
+// r2m = +inf disables (non-orthonormal axes, different points).
+struct alignas(64) BoundBall {
+  float center[4];
+  float a1[4], a2[4];  // orthonormal axes of plane A (its cylinders: radii bands 0-1); plane B is the complement
+  float r2m;
+  float band[8];       // [lo, hi] of d_A^2 for up to two plane-A radii, then of d_B^2 for plane-B radii
+  float pad[3];
+};
+
 // Everything final_light reads on its common paths (constant override, sky pre-test), in one 64-B block.
 struct alignas(64) HotSky {
   float sky[3];        // sky_light (shader.frag:405)
@@ -95,6 +116,8 @@ struct SceneAux {
   int32_t pad2_[2];
   HotSky hot_sky;
   SphereCull sphere_cull[RT4_MAX_SPHERES];
+  BoundBall union_bound[RT4_MAX_UNIONS];
+  BoundBall tiger_bound[RT4_MAX_TIGERS];
   PrimEntry prims[MAX_PRIMS];
 };
 

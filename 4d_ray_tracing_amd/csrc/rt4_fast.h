@@ -263,6 +263,23 @@ __device__ __forceinline__ void for_count(int runtime_n, F&& body) {
   }
 }
 
+// True when the ray's line stays clear of a bounding ball (rt4_aux.h BoundBall): the group's exact test
+// would report no hit. One 32-B scalar load, three dots.
+#ifndef RT4_BOUND_SKIP
+#define RT4_BOUND_SKIP 1
+#endif
+__device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray) {
+  const f16v k = *reinterpret_cast<const f16v*>(&bb);  // centre, a1, a2, r2m, band[0..2]
+  const f16v m = *(reinterpret_cast<const f16v*>(&bb) + 1);  // band[3..7]
+  const V4 pc = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
+  const float a = dot(pc, pc), b = dot(pc, ray.drct), l2 = dot(ray.drct, ray.drct);
+  const float u1 = dot(pc, V4{k[4], k[5], k[6], k[7]}), u2 = dot(pc, V4{k[8], k[9], k[10], k[11]});
+  const float dB = fmaf_(u1, u1, u2 * u2), dA = a - dB;  // squared distances to plane B and plane A
+  const bool near_surface = (dA >= k[13] && dA <= k[14]) || (dA >= k[15] && dA <= m[0]) ||
+                            (dB >= m[1] && dB <= m[2]) || (dB >= m[3] && dB <= m[4]);
+  return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && (a - fmaf_(4e-6f, a, k[12])) * l2 > b * b;
+}
+
 // Flat primitive-table index of each group's first entry (rt4_aux.h SceneAux::prims order): compile-time
 // for exact-count shapes (the scene-shape check pins one union / hypercube / tiger), else read.
 struct PrimBases {
@@ -333,9 +350,11 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
                                B.cyl + static_cast<uint32_t>(i)),
                       inter);
     });
-  if (K & K_UNION) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
+  if (K & K_UNION)
+    if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
   if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, 0, B.cube, ray), inter);
-  if (K & K_TIGER) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
+  if (K & K_TIGER)
+    if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
   return inter;
 }
 

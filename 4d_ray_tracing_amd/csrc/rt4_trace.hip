@@ -782,6 +782,47 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     if (st == RT4_OK) st = make_divc(ctx, s.unions[i].cylinder2.r, &a->union_r[i][1], err, errlen);
     a->union_gt[i] = sqrt_gt_threshold(s.unions[i].cylinder2.r);
   }
+  // bounding balls (rt4_aux.h BoundBall): R^2 = max over faces (r_self^2 + gt of the filter)
+  // rA / rB: the radii of the cylinders around plane A (c1's axes) / plane B (c2's axes)
+  auto bound = [](const rt4_cylinder& c1, const rt4_cylinder& c2, double r2, const float rA[2], const float rB[2],
+                  BoundBall* b) {
+    std::memset(b, 0, sizeof *b);
+    std::memcpy(b->center, c1.point, sizeof b->center);
+    std::memcpy(b->a1, c1.axis1, sizeof b->a1);
+    std::memcpy(b->a2, c1.axis2, sizeof b->a2);
+    const float rr[4] = {rA[0], rA[1], rB[0], rB[1]};
+    for (int q = 0; q < 4; q++) {
+      const double r2q = static_cast<double>(rr[q]) * rr[q];
+      b->band[2 * q] = static_cast<float>(r2q * 0.99);
+      b->band[2 * q + 1] = static_cast<float>(r2q * 1.01);
+    }
+    b->r2m = INFINITY;
+    const float* ax[4] = {c1.axis1, c1.axis2, c2.axis1, c2.axis2};
+    bool ok = same4(c1.point, c2.point) && std::isfinite(r2);
+    for (int i = 0; i < 4 && ok; i++)
+      for (int j = i; j < 4 && ok; j++) {
+        double d = 0;
+        for (int k = 0; k < 4; k++) d += static_cast<double>(ax[i][k]) * ax[j][k];
+        ok = std::isfinite(d) && (i == j ? std::fabs(d - 1.0) <= 1e-6 : std::fabs(d) <= 1e-6);
+      }
+    for (int k = 0; k < 4 && ok; k++) ok = std::isfinite(c1.point[k]) && std::fabs(c1.point[k]) < 1e15f;
+    if (ok && r2 < 1e30) b->r2m = std::nextafter(static_cast<float>(r2 * (1.0 + 1e-3)), INFINITY);
+  };
+  for (int i = 0; i < s.n_unions; i++) {  // both filters use gt(cylinder2.r) (shader.frag:286,290)
+    const rt4_cylinders_union& u = s.unions[i];
+    const double g = sqrt_gt_threshold(u.cylinder2.r);
+    const double r1 = u.cylinder1.r, r2 = u.cylinder2.r;
+    const float rA[2] = {u.cylinder1.r, u.cylinder1.r}, rB[2] = {u.cylinder2.r, u.cylinder2.r};
+    bound(u.cylinder1, u.cylinder2, std::max(r1 * r1, r2 * r2) + g, rA, rB, &a->union_bound[i]);
+  }
+  for (int i = 0; i < s.n_tigers; i++) {
+    const rt4_tiger& t = s.tigers[i];
+    const double g1 = sqrt_gt_threshold(t.outer_cyl2.r), g2 = sqrt_gt_threshold(t.outer_cyl1.r);
+    const double o1 = std::max(std::fabs(t.inner_cyl1.r), std::fabs(t.outer_cyl1.r));
+    const double o2 = std::max(std::fabs(t.inner_cyl2.r), std::fabs(t.outer_cyl2.r));
+    const float rA[2] = {t.inner_cyl1.r, t.outer_cyl1.r}, rB[2] = {t.inner_cyl2.r, t.outer_cyl2.r};
+    bound(t.inner_cyl1, t.inner_cyl2, std::max(o1 * o1 + g1, o2 * o2 + g2), rA, rB, &a->tiger_bound[i]);
+  }
   for (int i = 0; i < s.n_tigers && st == RT4_OK; i++) {
     const rt4_tiger& t = s.tigers[i];
     const float rs[4] = {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r};

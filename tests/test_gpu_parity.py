@@ -199,6 +199,50 @@ def test_find_intersection_grazing_spheres(rt4, oracle, name):
     assert ((c[:, 0] > 0) & ~on_space).mean() > 0.05
 
 
+def on_cylinder_rays(cyls, n, seed):
+    """Rays starting on (or within 1e-6 relative of) infinite cylinders (point, axis1, axis2, r), at any
+    distance along their axes: the cases where the exact test can report a NaN-distance hit (a negative
+    rounding under the sqrt) far from the figure's bounding ball."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(n):
+        cp, a1, a2, r = cyls[k % len(cyls)]
+        cp, a1, a2 = (np.array(v, np.float64) for v in (cp, a1, a2))
+        basis = np.linalg.qr(np.stack([a1, a2] + list(rng.normal(size=(2, 4)))).T)[0].T  # a1, a2, b1, b2
+        b1, b2 = basis[2], basis[3]
+        phi = rng.uniform(0, 2 * np.pi)
+        rr = r * (1 + rng.choice([0.0, 1e-7, -1e-7, 1e-6]))
+        p = cp + rng.uniform(-6, 6) * a1 + rng.uniform(-6, 6) * a2 + rr * (np.cos(phi) * b1 + np.sin(phi) * b2)
+        d = rng.normal(size=4)
+        d /= np.linalg.norm(d)
+        out.append(np.concatenate([p, d]))
+    return np.array(out, np.float32)
+
+
+@pytest.mark.parametrize("name", ["tiger", "cylinder4d", "all_primitives", "tiger_two_mirrors"])
+def test_find_intersection_rays_on_infinite_cylinders(rt4, oracle, name):
+    """Bit-exact on rays from the tiger's / union's cylinder surfaces, including NaN-distance hits
+    outside the bounding ball that the kernel's bound skip must not drop (rt4_aux.h BoundBall)."""
+    d = rt4.Scene.named(name).desc
+    cyls = []
+    for q in range(d.n_tigers):
+        t = d.tigers[q]
+        cyls += [(list(c.point), list(c.axis1), list(c.axis2), c.r) for c in (t.inner_cyl1, t.outer_cyl1, t.inner_cyl2,
+                                                                          t.outer_cyl2)]
+    for q in range(d.n_unions):
+        u = d.unions[q]
+        cyls += [(list(c.point), list(c.axis1), list(c.axis2), c.r) for c in (u.cylinder1, u.cylinder2)]
+    rays = on_cylinder_rays(cyls, 20000, 123)
+    c, cc = oracle.find_intersection(d, rays)
+    t = rt4.Tracer(device=0, scene=rt4.Scene(d))
+    try:
+        g, gc = t.debug_find_intersection(rays)
+    finally:
+        t.close()
+    assert_bits(g, c, f"{name} on-cylinder find_intersection")
+    assert_bits(gc, cc, f"{name} on-cylinder material color")
+
+
 # -------------------------------------------------------------------------------------- images
 def render_both(rt4, oracle, scene, u, reg, flags=0, old=None):
     t = rt4.Tracer(device=0, flags=flags, scene=scene)
