@@ -118,6 +118,12 @@ struct SceneAux {
   SphereCull sphere_cull[RT4_MAX_SPHERES];
   BoundBall union_bound[RT4_MAX_UNIONS];
   BoundBall tiger_bound[RT4_MAX_TIGERS];
+  // Hypercube (rt4_fast.h cube_cand): a face hit needs |q - c|^2 <= |cpt - c|^2 + 3 r^2 for the face
+  // square (orthonormal normal + axes); only center and r2m are used. A face that is not nearly
+  // parallel to the ray (cos_dn^2 >= 1e-12 |d|^2) has a finite hit point, so for a ray whose line
+  // clears the ball its extent test fails: skipped. Nearly parallel faces (the +inf / NaN "hits" of
+  // shader.frag:357-365) always run the exact test.
+  BoundBall hyper_bound[RT4_MAX_HYPERCUBES];
   PrimEntry prims[MAX_PRIMS];
 };
 

@@ -14,6 +14,9 @@
 #ifndef RT4_SPHERE_CULL
 #define RT4_SPHERE_CULL 1
 #endif
+#ifndef RT4_BOUND_SKIP
+#define RT4_BOUND_SKIP 1  // bounding-ball skips for tiger / union / hypercube faces (rt4_aux.h BoundBall)
+#endif
 
 namespace rt4 {
 
@@ -213,12 +216,14 @@ __device__ __forceinline__ Cand tiger_cand(const rt4_scene_desc* __restrict__ S,
   return closest(lo, hi);
 }
 
-__device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uint32_t id) {  // :352-366
+// far: the ray's line clears the hypercube's ball (rt4_aux.h hyper_bound); l2 = |drct|^2
+__device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uint32_t id, bool far, float l2) {  // :352-366
   const V4 cpt = ld4(c.point), cn = ld4(c.norm);
   const V4 vec_n = neg(cn);
   const float h = dot(sub(cpt, ray.point), vec_n);
   const float cos_dn = dot(ray.drct, vec_n);
   if (h < 0.0f || cos_dn < 0.0f) return no_cand();
+  if (far && cos_dn * cos_dn >= 1e-12f * l2) return no_cand();  // finite hit point, outside the ball
   const float dist = h / cos_dn;
   const V4 vec_cp = sub(mad(ray.drct, dist, ray.point), cpt);
   if (__builtin_fabsf(dot(vec_cp, ld4(c.x))) > c.r || __builtin_fabsf(dot(vec_cp, ld4(c.y))) > c.r ||
@@ -227,13 +232,24 @@ __device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uin
   return Cand{true, false, dist, 0.0f, id};
 }
 
-__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, int i, uint32_t base,
-                                               const Ray& ray) {  // :394-400
+__device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                               int i, uint32_t base, const Ray& ray) {  // :394-400
   const rt4_hypercube& hc = S->hypercubes[i];
+  float l2 = 0.0f;
+  bool far = false;
+#if RT4_BOUND_SKIP
+  {
+    const f16v k = *reinterpret_cast<const f16v*>(&X->hyper_bound[i]);  // centre 0-3, r2m 12
+    const V4 pc = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
+    const float a = dot(pc, pc), b = dot(pc, ray.drct);
+    l2 = dot(ray.drct, ray.drct);
+    far = a < 1e30f && l2 > 1e-30f && l2 < 1e30f && (a - fmaf_(4e-6f, a, k[12])) * l2 > b * b;
+  }
+#endif
   Cand res = no_cand();
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    if (!res.hit) res = cube_cand(hc.cubes[k], ray, base + k);
+    if (!res.hit) res = cube_cand(hc.cubes[k], ray, base + k, far, l2);
   }
   return res;
 }
@@ -265,9 +281,6 @@ __device__ __forceinline__ void for_count(int runtime_n, F&& body) {
 
 // True when the ray's line stays clear of a bounding ball (rt4_aux.h BoundBall): the group's exact test
 // would report no hit. One 32-B scalar load, three dots.
-#ifndef RT4_BOUND_SKIP
-#define RT4_BOUND_SKIP 1
-#endif
 __device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray) {
   const f16v k = *reinterpret_cast<const f16v*>(&bb);  // centre, a1, a2, r2m, band[0..2]
   const f16v m = *(reinterpret_cast<const f16v*>(&bb) + 1);  // band[3..7]
@@ -352,7 +365,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
     });
   if (K & K_UNION)
     if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, 0, B.cube, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, X, 0, B.cube, ray), inter);
   if (K & K_TIGER)
     if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
   return inter;

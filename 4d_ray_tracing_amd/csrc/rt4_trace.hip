@@ -823,6 +823,34 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     const float rA[2] = {t.inner_cyl1.r, t.outer_cyl1.r}, rB[2] = {t.inner_cyl2.r, t.outer_cyl2.r};
     bound(t.inner_cyl1, t.inner_cyl2, std::max(o1 * o1 + g1, o2 * o2 + g2), rA, rB, &a->tiger_bound[i]);
   }
+  for (int i = 0; i < s.n_hypercubes; i++) {  // rt4_aux.h hyper_bound
+    BoundBall& b = a->hyper_bound[i];
+    std::memset(&b, 0, sizeof b);
+    b.r2m = INFINITY;
+    double c[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 8; k++)
+      for (int q = 0; q < 4; q++) c[q] += s.hypercubes[i].cubes[k].point[q] / 8.0;
+    double r2 = 0, cmax = 0;
+    bool ok = true;
+    for (int k = 0; k < 8 && ok; k++) {
+      const rt4_cube& cu = s.hypercubes[i].cubes[k];
+      const float* v[4] = {cu.norm, cu.x, cu.y, cu.z};
+      for (int p = 0; p < 4 && ok; p++)
+        for (int q = p; q < 4 && ok; q++) {
+          double d = 0;
+          for (int m = 0; m < 4; m++) d += static_cast<double>(v[p][m]) * v[q][m];
+          ok = std::isfinite(d) && (p == q ? std::fabs(d - 1.0) <= 1e-6 : std::fabs(d) <= 1e-6);
+        }
+      double e = 0;
+      for (int q = 0; q < 4; q++) e += (cu.point[q] - c[q]) * (cu.point[q] - c[q]);
+      r2 = std::max(r2, e + 3.0 * cu.r * cu.r);
+      for (int q = 0; q < 4; q++) cmax = std::max(cmax, std::fabs(static_cast<double>(cu.point[q])));
+      ok = ok && std::isfinite(cu.r) && cu.r >= 0.0f && cmax < 1e15;
+    }
+    for (int q = 0; q < 4; q++) b.center[q] = static_cast<float>(c[q]);
+    // absolute coordinates round too: + (1e-5 max|coord|)^2
+    if (ok) b.r2m = std::nextafter(static_cast<float>(r2 * (1.0 + 1e-3) + 1e-10 * cmax * cmax), INFINITY);
+  }
   for (int i = 0; i < s.n_tigers && st == RT4_OK; i++) {
     const rt4_tiger& t = s.tigers[i];
     const float rs[4] = {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r};
