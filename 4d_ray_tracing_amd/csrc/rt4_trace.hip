@@ -35,7 +35,7 @@ using namespace rt4;
 namespace {
 
 #ifndef RT4_REFILL_MIN
-#define RT4_REFILL_MIN 8
+#define RT4_REFILL_MIN 1  // refill as soon as one lane is idle (A/B: 8 -> 1 is +4.5 % sphere, +6 % hypercube, +4 % tiger)
 #endif
 #ifndef RT4_LUT_PREFETCH
 // When the sampler-table entry of a possible diffuse bounce is fetched: 2 = at a hit, in flight
