@@ -61,7 +61,11 @@ __device__ __forceinline__ float sqrt_(float x) {
 #if RT4_FAST_SQRT
   // |x| in (0, 2^-96), denormals included, tested on the bit pattern: float compares may see a
   // denormal as zero
+#if RT4_FAST_SQRT == 2  // per-lane branch (exec-mask save/restore around both paths)
   if ((__float_as_uint(x) & 0x7FFFFFFFu) - 1u >= 0x0F7FFFFFu) return sqrt_core(x);
+#else  // wave-uniform branch: the library path only when some active lane needs it (scalar branch only)
+  if (!__any((__float_as_uint(x) & 0x7FFFFFFFu) - 1u < 0x0F7FFFFFu)) return sqrt_core(x);
+#endif
 #endif
   return __builtin_sqrtf(x);
 }
