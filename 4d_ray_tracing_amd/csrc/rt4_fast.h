@@ -20,6 +20,10 @@
 
 namespace rt4 {
 
+#ifdef RT4_LANESTATS
+__device__ unsigned long long* rt4_ls_counter;  // diagnostic build only: the launch's counter buffer
+#endif
+
 // x / b with the verified 3-op form when allowed (uniform branch: c.fast is a scene constant).
 __device__ __forceinline__ float div_c(float x, const DivC& c) {
   if (c.fast) {
@@ -339,6 +343,15 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
       pend |= skip ? 0u : (1u << i);
     });
     while (pend) {
+#ifdef RT4_LANESTATS  // diagnostic: pending-loop trips and their active lanes, per block in LDS
+      {
+        const unsigned long long ex = __builtin_amdgcn_read_exec();
+        if ((threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+          atomicAdd(rt4_ls_counter + 40, 1ull);
+          atomicAdd(rt4_ls_counter + 41, static_cast<unsigned long long>(__popcll(ex)));
+        }
+      }
+#endif
       const int i = __builtin_ctz(pend);
       pend &= pend - 1u;
       const uint32_t id = B.sphere + static_cast<uint32_t>(i);

@@ -321,6 +321,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
 
 #ifdef RT4_LANESTATS
   unsigned long long ls[20] = {};
+  rt4_ls_counter = counter;  // every thread stores the same pointer
 #endif
 #ifdef RT4_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;

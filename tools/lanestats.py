@@ -28,3 +28,6 @@ for p, n in enumerate(names):
     if n == "-" or e == 0:
         continue
     print(f"  {n:>30s}: {e:12d} wave execs ({e / max(c[16], 1):5.3f} per iteration), {l / e:5.1f} lanes avg")
+if c[40]:
+    print(f"  {'exact sphere test (pending)':>30s}: {c[40]:12d} wave execs ({c[40] / max(c[16], 1):5.3f} per iteration), "
+          f"{c[41] / c[40]:5.1f} lanes avg")
