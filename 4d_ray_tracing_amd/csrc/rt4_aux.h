@@ -124,6 +124,9 @@ struct SceneAux {
   // clears the ball its extent test fails: skipped. Nearly parallel faces (the +inf / NaN "hits" of
   // shader.frag:357-365) always run the exact test.
   BoundBall hyper_bound[RT4_MAX_HYPERCUBES];
+  // hypercube 0's cells as 6 float4 each {point, norm, x, y, z, {r}}, staged in LDS ahead of the
+  // primitive table so the pending-cell loop can read the cell a lane needs (rt4_fast.h)
+  float hyper_cells[8][24];
   PrimEntry prims[MAX_PRIMS];
 };
 

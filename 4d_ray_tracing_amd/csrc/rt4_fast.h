@@ -14,6 +14,10 @@
 #ifndef RT4_SPHERE_CULL
 #define RT4_SPHERE_CULL 1
 #endif
+#ifndef RT4_HYPER_PENDING
+#define RT4_HYPER_PENDING 1  // hypercube: per-lane pending-cell loop (hypercube_cand) instead of 8 cells in order
+#endif
+constexpr int HYPER_CELLS_LDS = 8 * 6;  // float4s of hypercube 0's cells staged ahead of the primitive table
 #ifndef RT4_BOUND_SKIP
 #define RT4_BOUND_SKIP 1  // bounding-ball skips for tiger / union / hypercube faces (rt4_aux.h BoundBall)
 #endif
@@ -236,8 +240,72 @@ __device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uin
   return Cand{true, false, dist, 0.0f, id};
 }
 
+__device__ __forceinline__ Cand hypercube_cand_seq(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                                   int i, uint32_t base, const Ray& ray);
+
+// cube_cand's exact test from a cell staged in LDS (rt4_aux.h hyper_cells): the same floats, the same ops
+__device__ __forceinline__ bool cell_hit(const float4* cell, const Ray& ray, float& dist) {
+  const float4 p4 = cell[0], n4 = cell[1], x4 = cell[2], y4 = cell[3], z4 = cell[4];
+  const float r = cell[5].x;
+  const V4 cpt{p4.x, p4.y, p4.z, p4.w};
+  const V4 vec_n = neg(V4{n4.x, n4.y, n4.z, n4.w});
+  const float h = dot(sub(cpt, ray.point), vec_n);
+  const float cos_dn = dot(ray.drct, vec_n);
+  dist = h / cos_dn;
+  const V4 vec_cp = sub(mad(ray.drct, dist, ray.point), cpt);
+  return !(__builtin_fabsf(dot(vec_cp, V4{x4.x, x4.y, x4.z, x4.w})) > r ||
+           __builtin_fabsf(dot(vec_cp, V4{y4.x, y4.y, y4.z, y4.w})) > r ||
+           __builtin_fabsf(dot(vec_cp, V4{z4.x, z4.y, z4.z, z4.w})) > r);
+}
+
+// hypercube_intersection (shader.frag:394-400) as two passes: every cell's cheap rejection
+// (h < 0 || cos_dn < 0, the far-face skip) for all lanes, then each lane's remaining candidate cells
+// in cell order until the first hit, read from LDS. Same first-hit-in-order result; a wave pays for
+// max-over-lanes(candidates tried) exact tests instead of all 8 cells.
+template <bool PENDING>
 __device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                               int i, uint32_t base, const Ray& ray) {  // :394-400
+                                               const float4* cells, int i, uint32_t base, const Ray& ray) {
+  if constexpr (PENDING) {
+    const rt4_hypercube& hc = S->hypercubes[i];
+    float l2 = 0.0f;
+    bool far = false;
+#if RT4_BOUND_SKIP
+    {
+      const f16v k = *reinterpret_cast<const f16v*>(&X->hyper_bound[i]);
+      const V4 pc = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
+      const float a = dot(pc, pc), b = dot(pc, ray.drct);
+      l2 = dot(ray.drct, ray.drct);
+      far = a < 1e30f && l2 > 1e-30f && l2 < 1e30f && (a - fmaf_(4e-6f, a, k[12])) * l2 > b * b;
+    }
+#endif
+    uint32_t cand = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const rt4_cube& c = hc.cubes[k];
+      const V4 vec_n = neg(ld4(c.norm));
+      const float h = dot(sub(ld4(c.point), ray.point), vec_n);
+      const float cos_dn = dot(ray.drct, vec_n);
+      const bool rejected = h < 0.0f || cos_dn < 0.0f || (far && cos_dn * cos_dn >= 1e-12f * l2);
+      cand |= rejected ? 0u : (1u << k);
+    }
+    Cand res = no_cand();
+    while (cand) {
+      const int k = __builtin_ctz(cand);
+      cand &= cand - 1u;
+      float dist;
+      if (cell_hit(cells + 6 * k, ray, dist)) {
+        res = Cand{true, false, dist, 0.0f, base + static_cast<uint32_t>(k)};
+        cand = 0u;
+      }
+    }
+    return res;
+  } else {
+    return hypercube_cand_seq(S, X, i, base, ray);
+  }
+}
+
+__device__ __forceinline__ Cand hypercube_cand_seq(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                                   int i, uint32_t base, const Ray& ray) {  // :394-400
   const rt4_hypercube& hc = S->hypercubes[i];
   float l2 = 0.0f;
   bool far = false;
@@ -378,7 +446,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
     });
   if (K & K_UNION)
     if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand(S, X, 0, B.cube, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
   if (K & K_TIGER)
     if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
   return inter;

@@ -296,14 +296,18 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   const int R = a.reflections_amount, NS = a.samples;
   const uint32_t useed = static_cast<uint32_t>(a.seed);
   // the primitive table (normals + materials of hits) is read per lane: stage it in LDS once
-  __shared__ float4 lds_prims[K == GENERIC ? 1 : n_prims_of(K) * 6];
+  // (+ hypercube 0's cells ahead of it, rt4_fast.h HYPER_CELLS_LDS)
+  constexpr int CELLS4 = (K != GENERIC && (K & K_HYPERCUBE)) ? HYPER_CELLS_LDS : 0;
+  __shared__ float4 lds_prims[K == GENERIC ? 1 : CELLS4 + n_prims_of(K) * 6];
   if constexpr (K != GENERIC) {
+    const float4* cells = reinterpret_cast<const float4*>(X->hyper_cells);
+    for (int t = threadIdx.x; t < CELLS4; t += blockDim.x) lds_prims[t] = cells[t];
     const float4* src = reinterpret_cast<const float4*>(X->prims);
     const int n4 = X->n_prims * 6;
-    for (int t = threadIdx.x; t < n4; t += blockDim.x) lds_prims[t] = src[t];
+    for (int t = threadIdx.x; t < n4; t += blockDim.x) lds_prims[CELLS4 + t] = src[t];
     __syncthreads();
   }
-  const PrimEntry* P = reinterpret_cast<const PrimEntry*>(lds_prims);
+  const PrimEntry* P = reinterpret_cast<const PrimEntry*>(lds_prims + CELLS4);
 
   unsigned b_next = 0, b_end = 0;  // wave-uniform: unclaimed part of the current batch
   bool exhausted = false;
@@ -824,6 +828,17 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     const float rA[2] = {t.inner_cyl1.r, t.outer_cyl1.r}, rB[2] = {t.inner_cyl2.r, t.outer_cyl2.r};
     bound(t.inner_cyl1, t.inner_cyl2, std::max(o1 * o1 + g1, o2 * o2 + g2), rA, rB, &a->tiger_bound[i]);
   }
+  for (int i = 0; i < 1 && i < s.n_hypercubes; i++)  // rt4_aux.h hyper_cells
+    for (int k = 0; k < 8; k++) {
+      const rt4_cube& cu = s.hypercubes[i].cubes[k];
+      float* d = a->hyper_cells[k];
+      std::memcpy(d, cu.point, 16);
+      std::memcpy(d + 4, cu.norm, 16);
+      std::memcpy(d + 8, cu.x, 16);
+      std::memcpy(d + 12, cu.y, 16);
+      std::memcpy(d + 16, cu.z, 16);
+      d[20] = cu.r;
+    }
   for (int i = 0; i < s.n_hypercubes; i++) {  // rt4_aux.h hyper_bound
     BoundBall& b = a->hyper_bound[i];
     std::memset(&b, 0, sizeof b);
