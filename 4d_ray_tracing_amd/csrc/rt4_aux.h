@@ -9,6 +9,7 @@
 //              RN(sqrt(.)) is monotone; gt/lt found by bisection over float bit patterns.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/rt4.h"
@@ -126,8 +127,11 @@ struct SceneAux {
   BoundBall hyper_bound[RT4_MAX_HYPERCUBES];
   // hypercube 0's cells as 6 float4 each {point, norm, x, y, z, {r}}, staged in LDS ahead of the
   // primitive table so the pending-cell loop can read the cell a lane needs (rt4_fast.h)
-  float hyper_cells[8][24];
+  float hyper_cells[8][24];  // must directly precede prims (kernels address it as prims - 48 float4)
   PrimEntry prims[MAX_PRIMS];
 };
+
+static_assert(offsetof(SceneAux, prims) - offsetof(SceneAux, hyper_cells) == sizeof(float) * 8 * 24,
+              "hyper_cells must directly precede prims");
 
 }  // namespace rt4

@@ -56,6 +56,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e.x; }
 using WEntry = float;
 __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #endif
+#ifndef RT4_ORDER_PREPASS
+#define RT4_ORDER_PREPASS 1  // longest-first tile order from a primary-ray pre-pass (rt4_tile_order_kernel)
+#endif
 #ifndef RT4_TILE_ORDER
 #define RT4_TILE_ORDER 0  // order the queue hands out a job's 8x8 tiles: 0 row-major from the top, 1 reversed
 #endif
@@ -234,6 +237,7 @@ struct KernelArgs {
   float focus[4];
   int32_t format, n_jobs;
   unsigned total;  // 64 x tiles of all jobs
+  const unsigned* order;  // queue position -> tile (rt4_tile_order_kernel), or null: row-major
   JobArgs jobs[RT4_MAX_SECTIONS];
 };
 
@@ -367,12 +371,12 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
           }
           const unsigned n = min(nidle - got, b_end - b_next);
           // a 64-pixel batch is one tile of one job: the job is wave-uniform here (scalar loads)
-          const unsigned btile = b_next >> 6;
+          const unsigned btile = a.order ? a.order[b_next >> 6] : (b_next >> 6);  // wave-uniform
           const int job = (a.n_jobs > 1 && btile >= a.jobs[1].tile_base) + (a.n_jobs > 2 && btile >= a.jobs[2].tile_base);
           const JobArgs& J = a.jobs[job];
           if (!active && rank >= got && rank < got + n) {
             const unsigned idx = b_next + (rank - got);
-            unsigned tile = (idx >> 6) - J.tile_base;
+            unsigned tile = btile - J.tile_base;
             const unsigned l = idx & 63u;
 #if RT4_TILE_ORDER == 1  // bottom-up: the last tiles handed out are the top rows
             tile = J.tiles_x * ((static_cast<unsigned>(J.reg.h) + 7u) >> 3) - 1u - tile;
@@ -600,18 +604,46 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const Scen
   }
 }
 
+// Tile order for the pixel queue (longest work first): one thread per 8x8 tile traces the primary ray
+// of the tile's centre pixel; tiles whose ray hits something go to the front of `order`, sky tiles to
+// the back. The queue hands tiles out in this order, so the slow tiles do not form the drain at the
+// end of the launch. Results do not depend on the order (every pixel is independent).
+template <uint32_t K>
+__global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                      const KernelArgs a, unsigned* __restrict__ order, unsigned* __restrict__ ends) {
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned n = a.total >> 6;
+  if (t >= n) return;
+  const int job = (a.n_jobs > 1 && t >= a.jobs[1].tile_base) + (a.n_jobs > 2 && t >= a.jobs[2].tile_base);
+  const JobArgs& J = a.jobs[job];
+  const unsigned lt = t - J.tile_base;
+  const int jj = min(static_cast<int>((lt % J.tiles_x) * 8u + 4u), J.reg.w - 1);
+  const int ii = min(static_cast<int>((lt / J.tiles_x) * 8u + 4u), J.reg.h - 1);
+  const float sx = (static_cast<float>(J.reg.x0 + jj) + 0.5f) / J.resolution[0];
+  const float sy = (static_cast<float>(region_row(J.reg, ii)) + 0.5f) / J.resolution[1];
+  const float mx = (sx - 0.5f) * J.mtr_sizes[0];
+  const float my = (0.5f - sy) * J.mtr_sizes[1];
+  V4 dd = mad(ld4(J.right_drct), mx, mad(ld4(J.top_drct), my, ld4(J.vec_to_mtr)));
+  dd = divs(dd, length(dd));
+  const typename Finder<K>::R c = Finder<K>::find(S, X, X->prims, Ray{ld4(a.focus), dd});
+  const unsigned pos = c.hit ? atomicAdd(ends, 1u) : n - 1u - atomicAdd(ends + 1, 1u);
+  order[pos] = t;
+}
+
 // ---------------------------------------------------------------- kernel table
 typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, unsigned long long*,
                         const WEntry*, unsigned*);
 typedef void (*FindFn)(const rt4_scene_desc*, const SceneAux*, const float*, float*, float*, int64_t);
+typedef void (*OrderFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, unsigned*, unsigned*);
 
 struct Variant {
   uint32_t shape;
   TraceFn trace[2];  // [lut]
   FindFn find;
+  OrderFn order;
 };
 
-#define RT4_VARIANT(K) {K, {rt4_trace_kernel<K, false>, rt4_trace_kernel<K, true>}, rt4_find_kernel<K>}
+#define RT4_VARIANT(K) {K, {rt4_trace_kernel<K, false>, rt4_trace_kernel<K, true>}, rt4_find_kernel<K>, rt4_tile_order_kernel<K>}
 // shape | (n_spaces+1) << 8 | (n_spheres+1) << 16 | (n_cylinders+1) << 24 (rt4_fast.h sh_count),
 // from the scene's object counts (the same encoding scene_shape() computes)
 #define SH(K, nsp, nsh, ncy) \
@@ -704,6 +736,11 @@ struct rt4_context {
   uint32_t shape = GENERIC;
   WEntry* d_wlut = nullptr;
   unsigned* d_queue = nullptr;  // QUEUE_SLOTS words
+  unsigned* d_order = nullptr;  // tile order (rt4_tile_order_kernel) + 2 end counters
+  size_t order_cap = 0;         // tiles it holds
+  hipEvent_t done = nullptr;    // recorded after each launch: launches on another stream wait for it
+  hipStream_t last_stream = nullptr;
+  bool launched = false;
   unsigned launch_seq = 0;
   int n_cu = 0;
 };
@@ -986,6 +1023,11 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (e == hipSuccess) e = hipMalloc(&c->d_scene, kSceneBytes);
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e == hipSuccess) {  // tile order for frames up to 2^18 tiles (16.7 M pixels); larger ones grow it once
+    e = hipMalloc(&c->d_order, ((size_t(1) << 18) + 2) * sizeof(unsigned));
+    if (e == hipSuccess) c->order_cap = size_t(1) << 18;
+  }
   if (e == hipSuccess && (flags & RT4_FLAG_SAMPLER_LUT)) {
     e = hipMalloc(&c->d_wlut, sizeof(WEntry) << 23);
     if (e == hipSuccess) {
@@ -1009,6 +1051,8 @@ void rt4_context_destroy(rt4_context* ctx) {
   if (ctx->d_scene) (void)hipFree(ctx->d_scene);
   if (ctx->d_wlut) (void)hipFree(ctx->d_wlut);
   if (ctx->d_queue) (void)hipFree(ctx->d_queue);
+  if (ctx->d_order) (void)hipFree(ctx->d_order);
+  if (ctx->done) (void)hipEventDestroy(ctx->done);
   if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
   delete ctx;
 }
@@ -1099,9 +1143,32 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   if (blocks < 1) blocks = 1;
   unsigned* q = ctx->d_queue + (ctx->launch_seq++ % QUEUE_SLOTS);
   HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
+  a.order = nullptr;
+  // The tile order buffer is one per context: a launch on another stream than the previous one
+  // waits for it (launches of one context run in submission order).
+  if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(s, ctx->done, 0));
+#if RT4_ORDER_PREPASS
+  if (ctx->order_cap < tiles) {  // a frame larger than any before: grow once (allocates)
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ctx->d_order) (void)hipFree(ctx->d_order);
+    ctx->d_order = nullptr;
+    ctx->order_cap = 0;
+    HIP_TRY(hipMalloc(&ctx->d_order, (static_cast<size_t>(tiles) + 2) * sizeof(unsigned)));
+    ctx->order_cap = tiles;
+  }
+  unsigned* ends = ctx->d_order + ctx->order_cap;
+  HIP_TRY(hipMemsetAsync(ends, 0, 2 * sizeof(unsigned), s));
+  hipLaunchKernelGGL(v.order, dim3((tiles + 255u) / 256u), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, ctx->d_order,
+                     ends);
+  HIP_TRY(hipGetLastError());
+  a.order = ctx->d_order;
+#endif
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, d_counter,
                      ctx->d_wlut, q);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->done, s));
+  ctx->last_stream = s;
+  ctx->launched = true;
   return RT4_OK;
 }
 

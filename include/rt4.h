@@ -315,7 +315,9 @@ typedef struct rt4_region {
  * Holds old_frame on entry and mix(old, new, part) on return (shader.frag:524-527).
  * d_counter (may be NULL): device uint64 incremented by the number of find_intersection calls
  * (one per ray-bounce, shader.frag:475). stream: hipStream_t (NULL = default stream).
- * Asynchronous: no host synchronisation, no allocation (graph-capture safe). */
+ * Asynchronous: no host synchronisation and no allocation for launches of up to 2^18 8x8 tiles
+ * (16.7 M pixels; a larger one grows the context's tile-order buffer once). Launches of one context
+ * run in submission order: a launch on another stream than the previous one waits for it. */
 int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
                       int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err,
                       size_t errlen);

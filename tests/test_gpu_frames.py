@@ -203,3 +203,35 @@ def test_sections_argument_checks_and_empty_job(rt4, oracle):
         assert bits_equal(fr.cpu().numpy(), c).all()
     finally:
         t.close()
+
+
+def test_launches_on_two_streams_and_a_large_frame(rt4, oracle):
+    """One context used from two streams (the tile-order buffer is shared: launches run in submission
+    order) and a frame above the preallocated 2^18 tiles (the buffer grows); images stay exact."""
+    import torch
+
+    scene = rt4.Scene.builtin("sphere")
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        u = rt4.make_uniforms(160, 100, samples=2, reflections=3, seed=9)
+        reg = rt4.region(160, 100)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        frames = [torch.zeros((100, 160, 4), device="cuda") for _ in range(4)]
+        for q, fr in enumerate(frames):
+            st = s1 if q % 2 == 0 else s2
+            t.render_device(u, reg, fr.data_ptr(), 160, 0, st.cuda_stream)
+        torch.cuda.synchronize()
+        c, _, _, _ = oracle.render(scene.desc, u, reg)
+        for fr in frames:
+            assert (fr.cpu().numpy().view(np.uint32) == c.view(np.uint32)).all()
+        # 4160 x 4104 pixels = 520 x 513 tiles > 2^18: grows the order buffer
+        W, H = 4160, 4104
+        ub = rt4.make_uniforms(W, H, samples=1, reflections=1, seed=9)
+        big = torch.zeros((H, W, 4), device="cuda")
+        t.render_device(ub, rt4.region(W, H), big.data_ptr(), W, 0, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        rows = rt4.region(W, 3, y0=H // 2)
+        cb, _, _, _ = oracle.render(scene.desc, ub, rows)
+        assert (big[H // 2:H // 2 + 3].cpu().numpy().view(np.uint32) == cb.view(np.uint32)).all()
+    finally:
+        t.close()
