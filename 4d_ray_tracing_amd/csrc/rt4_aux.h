@@ -114,6 +114,10 @@ struct SceneAux {
   float sky_pre_k;   // conservative sky pre-test (trace final_light): a <= 0 || a*a < l2 * sky_pre_k with
                      // a = dot(drct, sun.drct), l2 = dot(drct, drct) in [2^-40, 2^40] implies
                      // v_cos <= sky_c_star. sky_pre_k = RN(c*^2 len(sun)^2 (1 - 1e-5)); 0 disables.
+  // 1 when hypercube i's cells are axis-aligned in the canonical order: cell k's norm is +e_(k&3) for
+  // k < 4 and -e_(k&3) for k >= 4 (other components +-0), every |point| < 1e30. Then for finite rays
+  // (|p|, |d| < 1e30) the cull's dot products are exactly +-one component (rt4_fast.h hypercube_cand).
+  int32_t hyper_axis[RT4_MAX_HYPERCUBES];
   int32_t pad2_[2];
   HotSky hot_sky;
   SphereCull sphere_cull[RT4_MAX_SPHERES];

@@ -14,6 +14,12 @@
 #ifndef RT4_SPHERE_CULL
 #define RT4_SPHERE_CULL 1
 #endif
+#ifndef RT4_AXIS_ALL
+#define RT4_AXIS_ALL 0  // A/B only: the axis cull in the tiger-bearing kernels too (all_primitives: -4.5 %)
+#endif
+#ifndef RT4_HYPER_AXIS
+#define RT4_HYPER_AXIS 1  // hypercube cull: one-component form for axis-aligned canonical cells (rt4_aux.h hyper_axis)
+#endif
 #ifndef RT4_HYPER_PENDING
 #define RT4_HYPER_PENDING 1  // hypercube: per-lane pending-cell loop (hypercube_cand) instead of 8 cells in order
 #endif
@@ -262,7 +268,7 @@ __device__ __forceinline__ bool cell_hit(const float4* cell, const Ray& ray, flo
 // (h < 0 || cos_dn < 0, the far-face skip) for all lanes, then each lane's remaining candidate cells
 // in cell order until the first hit, read from LDS. Same first-hit-in-order result; a wave pays for
 // max-over-lanes(candidates tried) exact tests instead of all 8 cells.
-template <bool PENDING>
+template <bool PENDING, bool AXIS>
 __device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
                                                const float4* cells, int i, uint32_t base, const Ray& ray) {
   if constexpr (PENDING) {
@@ -278,15 +284,39 @@ __device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict_
       far = a < 1e30f && l2 > 1e-30f && l2 < 1e30f && (a - fmaf_(4e-6f, a, k[12])) * l2 > b * b;
     }
 #endif
+    // Axis-aligned canonical cells (rt4_aux.h hyper_axis) and a finite ray in every lane: vec_n is
+    // -+e_(k&3), so h = dot(cpt - p, vec_n) and cos_dn = dot(d, vec_n) are exactly -+(one component)
+    // (the other products are +-0, which leave a nonzero sum unchanged); only the sign of a zero
+    // result can differ, and the tests below do not see it (cos_dn enters squared).
+    bool axis = false;
+    if constexpr (AXIS)
+      axis = X->hyper_axis[i] != 0 &&
+             !__any(!(__builtin_fabsf(ray.point.x) < 1e30f && __builtin_fabsf(ray.point.y) < 1e30f &&
+                      __builtin_fabsf(ray.point.z) < 1e30f && __builtin_fabsf(ray.point.w) < 1e30f &&
+                      __builtin_fabsf(ray.drct.x) < 1e30f && __builtin_fabsf(ray.drct.y) < 1e30f &&
+                      __builtin_fabsf(ray.drct.z) < 1e30f && __builtin_fabsf(ray.drct.w) < 1e30f));
     uint32_t cand = 0;
+    if (axis) {
+      const float pc[4] = {ray.point.x, ray.point.y, ray.point.z, ray.point.w};
+      const float dc[4] = {ray.drct.x, ray.drct.y, ray.drct.z, ray.drct.w};
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const rt4_cube& c = hc.cubes[k];
-      const V4 vec_n = neg(ld4(c.norm));
-      const float h = dot(sub(ld4(c.point), ray.point), vec_n);
-      const float cos_dn = dot(ray.drct, vec_n);
-      const bool rejected = h < 0.0f || cos_dn < 0.0f || (far && cos_dn * cos_dn >= 1e-12f * l2);
-      cand |= rejected ? 0u : (1u << k);
+      for (int k = 0; k < 8; k++) {
+        const float d = hc.cubes[k].point[k & 3] - pc[k & 3];
+        const float h = k < 4 ? -d : d;
+        const float cos_dn = k < 4 ? -dc[k & 3] : dc[k & 3];
+        const bool rejected = h < 0.0f || cos_dn < 0.0f || (far && cos_dn * cos_dn >= 1e-12f * l2);
+        cand |= rejected ? 0u : (1u << k);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const rt4_cube& c = hc.cubes[k];
+        const V4 vec_n = neg(ld4(c.norm));
+        const float h = dot(sub(ld4(c.point), ray.point), vec_n);
+        const float cos_dn = dot(ray.drct, vec_n);
+        const bool rejected = h < 0.0f || cos_dn < 0.0f || (far && cos_dn * cos_dn >= 1e-12f * l2);
+        cand |= rejected ? 0u : (1u << k);
+      }
     }
     Cand res = no_cand();
     while (cand) {
@@ -446,7 +476,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
     });
   if (K & K_UNION)
     if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && (RT4_AXIS_ALL || !(K & K_TIGER))>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
   if (K & K_TIGER)
     if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
   return inter;

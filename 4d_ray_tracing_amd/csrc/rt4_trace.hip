@@ -895,6 +895,17 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
       std::memcpy(d + 16, cu.z, 16);
       d[20] = cu.r;
     }
+  for (int i = 0; i < s.n_hypercubes; i++) {  // rt4_aux.h hyper_axis
+    bool canon = true;
+    for (int k = 0; k < 8; k++) {
+      const rt4_cube& cu = s.hypercubes[i].cubes[k];
+      for (int q = 0; q < 4; q++) {
+        const float want = q != (k & 3) ? 0.0f : (k < 4 ? 1.0f : -1.0f);
+        canon = canon && cu.norm[q] == want && std::fabs(cu.point[q]) < 1e30f;  // -0 == 0
+      }
+    }
+    a->hyper_axis[i] = canon ? 1 : 0;
+  }
   for (int i = 0; i < s.n_hypercubes; i++) {  // rt4_aux.h hyper_bound
     BoundBall& b = a->hyper_bound[i];
     std::memset(&b, 0, sizeof b);

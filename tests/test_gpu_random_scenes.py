@@ -112,3 +112,25 @@ def test_random_scene_render(rt4, oracle, name, seed):
     fg, ng, fc, nc = render_both(rt4, oracle, scene, u, reg, flags=rt4.FLAG_SAMPLER_LUT)
     assert ng == nc
     assert_bits(fg, fc, f"{name}/{seed} image")
+
+
+@pytest.mark.parametrize("name", ["hypercube", "all_primitives"])
+def test_nonfinite_and_huge_rays(rt4, oracle, name):
+    """Rays with inf / NaN / |x| >= 1e30 components, one per 16 lanes: the hypercube's axis-aligned
+    cull (rt4_fast.h) must fall back to the full dot products for the whole wave."""
+    scene = rt4.Scene.named(name)
+    rays = random_rays(20000, 99)
+    rng = np.random.default_rng(3)
+    bad = np.arange(0, len(rays), 16)
+    vals = np.array([np.inf, -np.inf, np.nan, 1e30, -3e35, 1e-40], np.float32)
+    rays[bad, rng.integers(0, 8, len(bad))] = vals[rng.integers(0, len(vals), len(bad))]
+    rays[5000:5064, 4:8] = np.array([0.0, 0.0, 0.0, 1.0], np.float32)  # parallel to 6 of the 8 cells
+    rays[6000:6064, 0:4] = np.array([1e20, 2.0, 0.0, 0.0], np.float32)
+    c, cc = oracle.find_intersection(scene.desc, rays)
+    t = rt4.Tracer(device=0, scene=scene)
+    try:
+        g, gc = t.debug_find_intersection(rays)
+    finally:
+        t.close()
+    assert_bits(g, c, f"{name} non-finite rays")
+    assert_bits(gc, cc, f"{name} non-finite rays colour")
