@@ -278,8 +278,12 @@ template <uint32_t K, bool LUT>
 __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         unsigned long long* __restrict__ counter,
-                                                        const WEntry* __restrict__ wlut, unsigned* __restrict__ queue) {
+                                                        const WEntry* __restrict__ wlut, unsigned* __restrict__ queue,
+                                                        unsigned* __restrict__ queue_next) {
   const unsigned lane = threadIdx.x & 63u;
+  // the next launch's queue word starts at zero (launches of a context are ordered, launch_jobs):
+  // no memset between frames
+  if (blockIdx.x == 0 && threadIdx.x == 0) *queue_next = 0u;
   const unsigned total = a.total;
   const V4 focus = ld4(a.focus);
   const float indent = a.small_indent;
@@ -614,7 +618,7 @@ __global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, cons
 
 // ---------------------------------------------------------------- kernel table
 typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, unsigned long long*,
-                        const WEntry*, unsigned*);
+                        const WEntry*, unsigned*, unsigned*);
 typedef void (*FindFn)(const rt4_scene_desc*, const SceneAux*, const float*, float*, float*, int64_t);
 typedef void (*OrderFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, unsigned*, unsigned*);
 
@@ -739,7 +743,10 @@ struct rt4_context {
   hipStream_t last_stream = nullptr;
   bool launched = false;
   unsigned launch_seq = 0;
+  bool queue_dirty = false;  // a launch failed: the next one zeroes its queue word itself
   int n_cu = 0;
+  TraceFn occ_fn = nullptr;  // blocks per CU of the last trace kernel launched (occupancy query cache)
+  int occ_per_cu = 0;
 };
 
 #define HIP_TRY(expr)                                                                            \
@@ -1031,6 +1038,8 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (e == hipSuccess) e = hipMalloc(&c->d_scene, kSceneBytes);
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(c->d_queue, 0, QUEUE_SLOTS * sizeof(unsigned));
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream's first launch
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) {  // tile order for frames up to 2^18 tiles (16.7 M pixels); larger ones grow it once
     e = hipMalloc(&c->d_order, ((size_t(1) << 18) + 2) * sizeof(unsigned));
@@ -1145,13 +1154,16 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   const Variant& v = variant_for(ctx->shape);
   const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0];
   // grid: what the device holds at once; later blocks would only find the queue empty
-  int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), 256, 0));
+  if (ctx->occ_fn != fn) {
+    int n = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), 256, 0));
+    ctx->occ_fn = fn;
+    ctx->occ_per_cu = n;
+  }
+  const int per_cu = ctx->occ_per_cu;
   long long blocks = static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1);
   if (blocks > (static_cast<long long>(tiles) + 3) / 4) blocks = (static_cast<long long>(tiles) + 3) / 4;  // >= one tile per wave
   if (blocks < 1) blocks = 1;
-  unsigned* q = ctx->d_queue + (ctx->launch_seq++ % QUEUE_SLOTS);
-  HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
   a.order = nullptr;
   a.order_ends = nullptr;
   // The tile order buffer is one per context: a launch on another stream than the previous one
@@ -1182,8 +1194,15 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   a.order = ctx->d_order;
   a.order_ends = ends;
 #endif
+  unsigned* q = ctx->d_queue + (ctx->launch_seq % QUEUE_SLOTS);
+  unsigned* q_next = ctx->d_queue + (++ctx->launch_seq % QUEUE_SLOTS);  // zeroed by this launch
+  if (ctx->queue_dirty) {
+    HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
+    ctx->queue_dirty = false;
+  }
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, d_counter,
-                     ctx->d_wlut, q);
+                     ctx->d_wlut, q, q_next);
+  if (hipPeekAtLastError() != hipSuccess) ctx->queue_dirty = true;  // q_next may not be zeroed
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->done, s));
   ctx->last_stream = s;

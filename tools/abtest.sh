@@ -29,7 +29,7 @@ if [ "$cmd" = build ]; then
   done
 elif [ "$cmd" = run ]; then
   rounds=${1:-2}; shift || true
-  args=${*:-"--steps 30 --warmup 3 --no-cpu-baseline --no-reuse-leg"}
+  args=${*:-"--steps 30 --warmup 3 --no-cpu-baseline"}
   for r in $(seq 1 "$rounds"); do
     for so in "$VDIR"/*.so; do
       name=$(basename "$so" .so)
