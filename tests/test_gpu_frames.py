@@ -264,3 +264,32 @@ def test_tile_order_reuse_follows_scene_and_camera(rt4, oracle):
             assert (fr.cpu().numpy().view(np.uint32) == c.view(np.uint32)).all(), name
     finally:
         t.close()
+
+
+def test_queue_words_across_many_launches(rt4, oracle):
+    """Each launch zeroes the next launch's rotating queue word (64 words, no memset between frames):
+    150 launches, wrapping the words twice, on alternating streams with empty regions in between,
+    must each render the whole frame. Per-launch intersection counts and the last frame are checked
+    against the oracle."""
+    import torch
+
+    scene = rt4.Scene.builtin("sphere")
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        W, H = 40, 24
+        u = rt4.make_uniforms(W, H, samples=1, reflections=2, seed=31)
+        reg = rt4.region(W, H)
+        c, n_ref, _, _ = oracle.render(scene.desc, u, reg)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        fr = torch.zeros((H, W, 4), device="cuda")
+        counts = torch.zeros(150, dtype=torch.int64, device="cuda")
+        for q in range(150):
+            st = streams[(q // 7) % 2]
+            if q % 11 == 5:  # an empty region launches nothing and must not consume a queue word
+                t.render_device(u, rt4.region(0, 0), fr.data_ptr(), W, 0, st.cuda_stream)
+            t.render_device(u, reg, fr.data_ptr(), W, counts[q:].data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        assert counts.cpu().tolist() == [n_ref] * 150
+        assert (fr.cpu().numpy().view(np.uint32) == c.view(np.uint32)).all()
+    finally:
+        t.close()
