@@ -285,6 +285,32 @@ def test_render_bitwise_config3_rows(rt4, oracle):
     assert_bits(fg, fc, "config3 rows")
 
 
+def test_render_bitwise_config1_full_frame(rt4, oracle):
+    """BASELINE config 1 (sphere, 256x256, 1 spp, 2 bounces, seed 12345): every pixel, and the count
+    stays within the nominal bound W*H*spp*(B+1)."""
+    u = rt4.make_uniforms(256, 256, samples=1, reflections=2, seed=12345)
+    reg = rt4.region(256, 256)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.named("sphere"), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
+    assert ng == nc
+    assert 256 * 256 <= ng <= 256 * 256 * 1 * 3
+    assert_bits(fg, fc, "config1 frame")
+
+
+@pytest.mark.parametrize("name,spp,bounces,flags", [
+    ("tiger_two_mirrors", 64, 12, "lut"),  # BASELINE config 4 (3840x2160, 64 spp, 12 bounces)
+    ("all_primitives", 16, 8, "inline"),  # BASELINE config 5's frame (3840x2160, 16 spp per frame)
+])
+def test_render_bitwise_4k_configs_rows(rt4, oracle, name, spp, bounces, flags):
+    """The 8-GPU configs at their full 4K resolution and sample counts, on two rows far apart (one
+    near the middle, one in the lower half): uniforms and scr_coord bits are those of the 4K frame."""
+    u = rt4.make_uniforms(3840, 2160, samples=spp, reflections=bounces, seed=12345)
+    reg = rt4.region(3840, 2, y0=1003, band_rows=1, band_step=700)
+    f = {"lut": rt4.FLAG_SAMPLER_LUT, "inline": 0}[flags]
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene.named(name), u, reg, flags=f)
+    assert ng == nc
+    assert_bits(fg, fc, f"{name} 4k rows")
+
+
 def test_progressive_blend(rt4, oracle):
     """mix(old_frame, new, part) with part = 1/3 over a non-zero old frame (shader.frag:524-527)."""
     u = rt4.make_uniforms(64, 40, samples=2, reflections=3, seed=99, part=1.0 / 3.0)
