@@ -519,7 +519,7 @@ int rt4_progressive_uniforms(const rt4_uniforms* base, uint32_t frame_number, rt
 }
 
 const char* rt4_build_info(void) {
-  return "rt4 0.1 target=gfx950 fp32-contract=off div/sqrt=correctly-rounded built " __DATE__;
+  return "rt4 0.2 " RT4_KERNEL_VERSION " target=gfx950 fp32-contract=off div/sqrt=correctly-rounded built " __DATE__;
 }
 
 }  // extern "C"

@@ -21,8 +21,11 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <map>
+#include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/rt4.h"
 #include "rt4_device_math.h"
@@ -499,19 +502,46 @@ __global__ void rt4_build_wlut_kernel(WEntry* __restrict__ lut) {
   lut[m] = w;
 }
 
-// Exhaustive check of div_c against the IEEE quotient for every 32-bit numerator pattern.
-__global__ void rt4_verify_div_kernel(float b, float y, unsigned* __restrict__ mismatches) {
-  const DivC c{b, y, 1, 0};
+// Checks of the verified-divisor quotient div_c (rt4_fast.h) against the IEEE quotient x / b, one
+// divisor per blockIdx.y. Equivalent to all 2^32 numerators at a fraction of the work (DESIGN.md
+// §4.5): both quotients are odd in x (RN is symmetric), so only sign-0 patterns are swept; and in the
+// middle band of exponent fields [lo, hi] every intermediate (x, q, the exact residual x - q b when
+// non-zero, q2, x / b) is a normal number, so scaling x by 2^k scales every rounded step exactly and
+// one field stands for the whole band. The band is swept at three representative fields (lo, mid,
+// hi); every field outside it, subnormals, zero, inf and NaN included, is swept in full.
+// lo > hi: no band, all 256 fields.
+struct DivSweep {
+  float b, y;
+  uint32_t lo, hi;
+};
+constexpr int MAX_DIV_SWEEPS = 128;
+struct DivSweeps {
+  DivSweep d[MAX_DIV_SWEEPS];
+};
+__device__ __forceinline__ uint32_t div_sweep_fields(const DivSweep& d) {
+  return d.lo > d.hi ? 256u : d.lo + 3u + (255u - d.hi);
+}
+__device__ __forceinline__ uint32_t div_sweep_field(const DivSweep& d, uint32_t k) {
+  if (d.lo > d.hi || k < d.lo) return k;
+  k -= d.lo;
+  if (k < 3u) return k == 0u ? d.lo : (k == 1u ? (d.lo + d.hi) / 2u : d.hi);
+  return d.hi + 1u + (k - 3u);
+}
+__global__ void rt4_verify_div_kernel(const DivSweeps sw, unsigned* __restrict__ mismatches) {
+  const DivSweep d = sw.d[blockIdx.y];
+  const DivC c{d.b, d.y, 1, 0};
+  const uint64_t total = static_cast<uint64_t>(div_sweep_fields(d)) << 23;
   unsigned bad = 0;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
-    const float x = __uint_as_float(static_cast<uint32_t>(i));
-    const float q1 = x / b;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const uint32_t f = div_sweep_field(d, static_cast<uint32_t>(i >> 23));
+    const float x = __uint_as_float((f << 23) | (static_cast<uint32_t>(i) & 0x007FFFFFu));
+    const float q1 = x / d.b;
     const float q2 = div_c(x, c);
     const bool same = __float_as_uint(q1) == __float_as_uint(q2) || (q1 != q1 && q2 != q2);
     bad += same ? 0u : 1u;
   }
-  if (bad) atomicAdd(mismatches, bad);
+  if (bad) atomicAdd(mismatches + blockIdx.y, bad);
 }
 
 // Exhaustive check of sqrt_ (rt4_device_math.h) against the IEEE square root for every 32-bit pattern.
@@ -526,16 +556,20 @@ __global__ void rt4_verify_sqrt_kernel(unsigned long long* __restrict__ mismatch
   if (bad) atomicAdd(mismatches, static_cast<unsigned long long>(bad));
 }
 
-// min over all float patterns c with acos_(c) < ang, as an order-preserving key (0xFFFFFFFF: none)
+// min over the float patterns c in [lo, lo + count) with acos_(c) < ang, as an order-preserving key
+// (0xFFFFFFFF: none). For ang <= 1 only c in (0.5, 1] can qualify: acos_ of c <= 0.5 is >= pi/3 - tiny
+// (rt4_device_math.h acos_: the small branch returns pi/2 - asin_core(c), the big negative one
+// pi - 2 asin_core >= pi/2), and NaN for NaN or c > 1. rt4_debug_sky_threshold(1.0, full) > 0.5 proves
+// it over all 2^32 patterns (tests/test_gpu_parity.py).
 __device__ __forceinline__ uint32_t order_key(float f) {
   const uint32_t b = __float_as_uint(f);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
-__global__ void rt4_sky_threshold_kernel(float ang, uint32_t* __restrict__ best) {
+__global__ void rt4_sky_threshold_kernel(float ang, uint32_t lo, uint64_t count, uint32_t* __restrict__ best) {
   uint32_t mine = 0xFFFFFFFFu;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
-    const float c = __uint_as_float(static_cast<uint32_t>(i));
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count; i += stride) {
+    const float c = __uint_as_float(lo + static_cast<uint32_t>(i));
     if (acos_(c) < ang) mine = min(mine, order_key(c));
   }
   if (mine != 0xFFFFFFFFu) atomicMin(best, mine);
@@ -729,8 +763,7 @@ struct rt4_context {
   uint32_t flags = 0;
   rt4_scene_desc* d_scene = nullptr;  // followed by its SceneAux (scene_aux())
   SceneAux aux{};
-  unsigned* d_scratch = nullptr;      // verification counter
-  std::map<uint32_t, bool> div_ok;   // verified divisors (by bit pattern)
+  unsigned* d_scratch = nullptr;      // verification counters (MAX_DIV_SWEEPS + 1 words)
   bool has_scene = false;
   uint32_t shape = GENERIC;
   WEntry* d_wlut = nullptr;
@@ -789,32 +822,112 @@ float sqrt_lt_threshold(float r) {
   return fbits(hi);
 }
 
-int make_divc(rt4_context* ctx, float b, DivC* out, char* err, size_t errlen) {
-  DivC d{b, 1.0f / b, 0, 0};
-  uint32_t key;
-  std::memcpy(&key, &b, 4);
-  auto it = ctx->div_ok.find(key);
-  if (it == ctx->div_ok.end()) {
-    bool ok = false;
-    if (std::isfinite(b) && b != 0.0f && std::isfinite(d.y)) {
-      HIP_TRY(hipMemset(ctx->d_scratch, 0, sizeof(unsigned)));
-      hipLaunchKernelGGL(rt4_verify_div_kernel, dim3(65536), dim3(256), 0, 0, b, d.y, ctx->d_scratch);
-      HIP_TRY(hipGetLastError());
-      unsigned bad = 1;
-      HIP_TRY(hipMemcpy(&bad, ctx->d_scratch, sizeof(unsigned), hipMemcpyDeviceToHost));
-      ok = bad == 0;
-    }
-    it = ctx->div_ok.emplace(key, ok).first;
+// Verified scene constants, process-wide (a pure function of the fp32 bit patterns and of this
+// library's device code, the same on every gfx950): divisor bits -> div_c exact for all numerators;
+// sun angular-size bits -> the sky-threshold search result (order key, 0xFFFFFFFF: none).
+std::mutex g_verify_mu;
+std::map<uint32_t, bool> g_div_ok;
+std::map<uint32_t, uint32_t> g_sky_best;
+
+uint32_t fkey(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+
+bool divisor_candidate(float b) { return std::isfinite(b) && b != 0.0f && std::isfinite(1.0f / b); }
+
+// The middle band of exponent fields of rt4_verify_div_kernel for divisor b (lo > hi: none). x = m 2^e
+// (field e + 127): the exact residual x - q b is a multiple of 2^(e - 47), so it is zero or normal for
+// e >= -79; q, q2 and x / b (exponent e - eb + {-1, 0, 1}) stay normal and finite for
+// -125 + eb <= e <= 126 + eb. Four fields of margin on each side; fields 251-255 always swept.
+DivSweep div_sweep(float b, bool full) {
+  DivSweep d{b, 1.0f / b, 1u, 0u};
+  if (full) return d;
+  int eb = 0;
+  std::frexp(b, &eb);
+  eb -= 1;  // b = 1.m * 2^eb
+  const int e_lo = std::max(-79, -125 + eb) + 4, e_hi = std::min(122, 126 + eb) - 4;
+  if (e_lo <= e_hi) {
+    d.lo = static_cast<uint32_t>(e_lo + 127);
+    d.hi = static_cast<uint32_t>(e_hi + 127);
   }
-  d.fast = it->second ? 1 : 0;
-  *out = d;
+  return d;
+}
+
+// Verifies the divisors and the sky threshold not yet in the caches: one launch for all divisors, one
+// for the threshold, one copy back.
+int verify_constants(rt4_context* ctx, const std::vector<float>& divisors, bool need_sky, float ang, char* err,
+                     size_t errlen) {
+  std::lock_guard<std::mutex> lock(g_verify_mu);
+  DivSweeps sw;
+  std::memset(&sw, 0, sizeof sw);
+  std::vector<uint32_t> todo;
+  for (float b : divisors) {
+    const uint32_t k = fkey(b);
+    if (!divisor_candidate(b) || g_div_ok.count(k) || std::find(todo.begin(), todo.end(), k) != todo.end()) continue;
+    if (todo.size() == static_cast<size_t>(MAX_DIV_SWEEPS)) break;  // the rest stays on IEEE division
+    sw.d[todo.size()] = div_sweep(b, false);
+    todo.push_back(k);
+  }
+  const bool sky = need_sky && !g_sky_best.count(fkey(ang));
+  if (todo.empty() && !sky) return RT4_OK;
+  const size_t n = todo.size();
+  std::vector<uint32_t> res(n + 1, 0u);
+  res[n] = 0xFFFFFFFFu;
+  HIP_TRY(hipMemcpy(ctx->d_scratch, res.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (n) {
+    hipLaunchKernelGGL(rt4_verify_div_kernel, dim3(2048, static_cast<unsigned>(n)), dim3(256), 0, 0, sw, ctx->d_scratch);
+    HIP_TRY(hipGetLastError());
+  }
+  if (sky) {
+    const bool small = ang <= 1.0f;  // only c in (0.5, 1] can have acos_(c) < ang (rt4_sky_threshold_kernel)
+    const uint32_t lo = small ? 0x3F000001u : 0u;
+    const uint64_t count = small ? (0x3F800000ull - 0x3F000001ull + 1ull) : (1ull << 32);
+    hipLaunchKernelGGL(rt4_sky_threshold_kernel, dim3(small ? 512 : 65536), dim3(256), 0, 0, ang, lo, count,
+                       ctx->d_scratch + n);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpy(res.data(), ctx->d_scratch, (n + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; i++) g_div_ok[todo[i]] = res[i] == 0u;
+  if (sky) g_sky_best[fkey(ang)] = res[n];
   return RT4_OK;
+}
+
+DivC make_divc(float b) {
+  DivC d{b, 1.0f / b, 0, 0};
+  if (divisor_candidate(b)) {
+    std::lock_guard<std::mutex> lock(g_verify_mu);
+    auto it = g_div_ok.find(fkey(b));
+    d.fast = (it != g_div_ok.end() && it->second) ? 1 : 0;
+  }
+  return d;
+}
+
+// length(sun.drct) exactly as the device computes it (rt4_device_math.h dot/length)
+float sun_length(const rt4_scene_desc& s) {
+  const float* d = s.sun.drct;
+  return std::sqrt(std::fmaf(d[3], d[3], std::fmaf(d[2], d[2], std::fmaf(d[1], d[1], d[0] * d[0]))));
 }
 
 int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err, size_t errlen) {
   std::memset(a, 0, sizeof *a);
+  {
+    std::vector<float> divs;
+    for (int i = 0; i < s.n_spheres; i++) divs.push_back(s.spheres[i].r);
+    for (int i = 0; i < s.n_cylinders; i++) divs.push_back(s.cylinders[i].r);
+    for (int i = 0; i < s.n_unions; i++) {
+      divs.push_back(s.unions[i].cylinder1.r);
+      divs.push_back(s.unions[i].cylinder2.r);
+    }
+    for (int i = 0; i < s.n_tigers; i++) {
+      const rt4_tiger& t = s.tigers[i];
+      for (float r : {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r}) divs.push_back(r);
+    }
+    divs.push_back(s.sun.angular_size);
+    divs.push_back(sun_length(s));
+    const int vs = verify_constants(ctx, divs, s.final_light_mode == RT4_FINAL_LIGHT_SUN_SKY, s.sun.angular_size, err,
+                                    errlen);
+    if (vs != RT4_OK) return vs;
+  }
   int st = RT4_OK;
-  for (int i = 0; i < s.n_spheres && st == RT4_OK; i++) st = make_divc(ctx, s.spheres[i].r, &a->sphere_r[i], err, errlen);
+  for (int i = 0; i < s.n_spheres; i++) a->sphere_r[i] = make_divc(s.spheres[i].r);
   for (int i = 0; i < s.n_spheres; i++) {  // rt4_aux.h SphereCull
     const float r = s.spheres[i].r;
     std::memcpy(a->sphere_cull[i].center, s.spheres[i].center, sizeof a->sphere_cull[i].center);
@@ -822,10 +935,10 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     const bool ok = r >= 1e-15f && r <= 1e15f;  // r <= 0: sin_oap < 1 always, never cull
     a->sphere_cull[i].r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
   }
-  for (int i = 0; i < s.n_cylinders && st == RT4_OK; i++) st = make_divc(ctx, s.cylinders[i].r, &a->cyl_r[i], err, errlen);
-  for (int i = 0; i < s.n_unions && st == RT4_OK; i++) {
-    st = make_divc(ctx, s.unions[i].cylinder1.r, &a->union_r[i][0], err, errlen);
-    if (st == RT4_OK) st = make_divc(ctx, s.unions[i].cylinder2.r, &a->union_r[i][1], err, errlen);
+  for (int i = 0; i < s.n_cylinders; i++) a->cyl_r[i] = make_divc(s.cylinders[i].r);
+  for (int i = 0; i < s.n_unions; i++) {
+    a->union_r[i][0] = make_divc(s.unions[i].cylinder1.r);
+    a->union_r[i][1] = make_divc(s.unions[i].cylinder2.r);
     a->union_gt[i] = sqrt_gt_threshold(s.unions[i].cylinder2.r);
   }
   // bounding balls (rt4_aux.h BoundBall): R^2 = max over faces (r_self^2 + gt of the filter)
@@ -919,23 +1032,22 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     // absolute coordinates round too: + (1e-5 max|coord|)^2
     if (ok) b.r2m = std::nextafter(static_cast<float>(r2 * (1.0 + 1e-3) + 1e-10 * cmax * cmax), INFINITY);
   }
-  for (int i = 0; i < s.n_tigers && st == RT4_OK; i++) {
+  for (int i = 0; i < s.n_tigers; i++) {
     const rt4_tiger& t = s.tigers[i];
     const float rs[4] = {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r};
-    for (int k = 0; k < 4 && st == RT4_OK; k++) st = make_divc(ctx, rs[k], &a->tiger_r[i][k], err, errlen);
+    for (int k = 0; k < 4; k++) a->tiger_r[i][k] = make_divc(rs[k]);
     a->tiger_gt[i][0] = sqrt_gt_threshold(t.outer_cyl2.r);
     a->tiger_lt[i][0] = sqrt_lt_threshold(t.inner_cyl2.r);
     a->tiger_gt[i][1] = sqrt_gt_threshold(t.outer_cyl1.r);
     a->tiger_lt[i][1] = sqrt_lt_threshold(t.inner_cyl1.r);
   }
-  if (st == RT4_OK) st = make_divc(ctx, s.sun.angular_size, &a->sun_ang, err, errlen);
-  if (st == RT4_OK && s.final_light_mode == RT4_FINAL_LIGHT_SUN_SKY) {  // sky threshold (rt4_aux.h)
-    const uint32_t init = 0xFFFFFFFFu;
-    HIP_TRY(hipMemcpy(ctx->d_scratch, &init, sizeof init, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(rt4_sky_threshold_kernel, dim3(65536), dim3(256), 0, 0, s.sun.angular_size, ctx->d_scratch);
-    HIP_TRY(hipGetLastError());
-    uint32_t best = 0;
-    HIP_TRY(hipMemcpy(&best, ctx->d_scratch, sizeof best, hipMemcpyDeviceToHost));
+  a->sun_ang = make_divc(s.sun.angular_size);
+  if (s.final_light_mode == RT4_FINAL_LIGHT_SUN_SKY) {  // sky threshold (rt4_aux.h), verify_constants
+    uint32_t best;
+    {
+      std::lock_guard<std::mutex> lock(g_verify_mu);
+      best = g_sky_best.at(fkey(s.sun.angular_size));
+    }
     if (best == 0xFFFFFFFFu) {
       a->sky_c_star = INFINITY;  // acos never below the angular size: always sky
     } else {
@@ -947,10 +1059,9 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
   } else {
     a->sky_c_star = -INFINITY;
   }
-  if (st == RT4_OK) {  // length(sun.drct) exactly as the device computes it (rt4_device_math.h dot/length)
-    const float* d = s.sun.drct;
-    const float len = std::sqrt(std::fmaf(d[3], d[3], std::fmaf(d[2], d[2], std::fmaf(d[1], d[1], d[0] * d[0]))));
-    st = make_divc(ctx, len, &a->sun_len, err, errlen);
+  if (st == RT4_OK) {
+    const float len = sun_length(s);
+    a->sun_len = make_divc(len);
     // Sky pre-test constant (rt4_aux.h sky_pre_k). With a*a < l2*K computed in fp32 (3 roundings) the
     // exact ratio a / (sqrt(l2) len) is below c* (1 - 4.9e-6); the kernel's v_cos (3 more roundings)
     // stays below c* (1 - 4.6e-6) <= c*, i.e. the sky branch. Needs c* > 0 and K well inside the
@@ -1036,7 +1147,7 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   c->flags = flags;
   hipError_t e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e == hipSuccess) e = hipMalloc(&c->d_scene, kSceneBytes);
-  if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc(&c->d_scratch, (MAX_DIV_SWEEPS + 1) * sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess) e = hipMemset(c->d_queue, 0, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream's first launch
@@ -1081,6 +1192,8 @@ int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* e
   HIP_TRY(hipSetDevice(ctx->device));
   st = build_aux(ctx, *scene, &ctx->aux, err, errlen);
   if (st != RT4_OK) return st;
+  // A frame still in flight on a caller's (non-blocking) stream reads d_scene: let it finish first.
+  if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
   HIP_TRY(hipMemcpy(ctx->d_scene, scene, sizeof(rt4_scene_desc), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(reinterpret_cast<char*>(ctx->d_scene) + kAuxOffset, &ctx->aux, sizeof(SceneAux),
                     hipMemcpyHostToDevice));
@@ -1200,13 +1313,24 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
     HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
     ctx->queue_dirty = false;
   }
+  (void)hipGetLastError();  // a sticky error of an earlier, unrelated call must not be taken for this launch's
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, d_counter,
                      ctx->d_wlut, q, q_next);
-  if (hipPeekAtLastError() != hipSuccess) ctx->queue_dirty = true;  // q_next may not be zeroed
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ctx->done, s));
+  const hipError_t le = hipGetLastError();
+  // Record the event whatever happened: a launch that may have been enqueued still orders the next
+  // launch on another stream behind it (they share d_order / the queue words).
+  const hipError_t re = hipEventRecord(ctx->done, s);
   ctx->last_stream = s;
   ctx->launched = true;
+  if (le != hipSuccess) {
+    ctx->queue_dirty = true;  // q_next may not be zeroed
+    rt4_set_err(err, errlen, "trace kernel launch failed: %s", hipGetErrorString(le));
+    return RT4_ERR_HIP;
+  }
+  if (re != hipSuccess) {
+    rt4_set_err(err, errlen, "hipEventRecord failed: %s", hipGetErrorString(re));
+    return RT4_ERR_HIP;
+  }
   return RT4_OK;
 }
 
@@ -1328,6 +1452,44 @@ int rt4_debug_verify_sqrt(rt4_context* ctx, uint64_t* mismatches, char* err, siz
   (void)hipFree(d);
   if (e != hipSuccess) return rt4_set_err(err, errlen, "verify_sqrt failed: %s", hipGetErrorString(e)), RT4_ERR_HIP;
   *mismatches = v;
+  return RT4_OK;
+}
+
+int rt4_debug_verify_div(rt4_context* ctx, float b, int32_t full, uint64_t* mismatches, char* err, size_t errlen) {
+  if (!ctx || !mismatches) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  if (!divisor_candidate(b)) return rt4_set_err(err, errlen, "divisor %g has no finite reciprocal", b), RT4_ERR_ARG;
+  HIP_TRY(hipSetDevice(ctx->device));
+  std::lock_guard<std::mutex> lock(g_verify_mu);  // d_scratch is shared with verify_constants
+  DivSweeps sw;
+  std::memset(&sw, 0, sizeof sw);
+  sw.d[0] = div_sweep(b, full != 0);
+  HIP_TRY(hipMemset(ctx->d_scratch, 0, sizeof(unsigned)));
+  hipLaunchKernelGGL(rt4_verify_div_kernel, dim3(8192, 1), dim3(256), 0, 0, sw, ctx->d_scratch);
+  HIP_TRY(hipGetLastError());
+  unsigned v = 0;
+  HIP_TRY(hipMemcpy(&v, ctx->d_scratch, sizeof v, hipMemcpyDeviceToHost));
+  *mismatches = v;
+  return RT4_OK;
+}
+
+int rt4_debug_sky_threshold(rt4_context* ctx, float ang, int32_t full, float* c_min, char* err, size_t errlen) {
+  if (!ctx || !c_min) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  HIP_TRY(hipSetDevice(ctx->device));
+  std::lock_guard<std::mutex> lock(g_verify_mu);
+  const bool small = !full && ang <= 1.0f;
+  const uint32_t init = 0xFFFFFFFFu, lo = small ? 0x3F000001u : 0u;
+  const uint64_t count = small ? (0x3F800000ull - 0x3F000001ull + 1ull) : (1ull << 32);
+  HIP_TRY(hipMemcpy(ctx->d_scratch, &init, sizeof init, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(rt4_sky_threshold_kernel, dim3(small ? 512 : 65536), dim3(256), 0, 0, ang, lo, count, ctx->d_scratch);
+  HIP_TRY(hipGetLastError());
+  uint32_t best = 0;
+  HIP_TRY(hipMemcpy(&best, ctx->d_scratch, sizeof best, hipMemcpyDeviceToHost));
+  if (best == 0xFFFFFFFFu) {
+    *c_min = NAN;
+  } else {
+    const uint32_t bits = (best & 0x80000000u) ? (best & 0x7FFFFFFFu) : ~best;
+    std::memcpy(c_min, &bits, 4);
+  }
   return RT4_OK;
 }
 

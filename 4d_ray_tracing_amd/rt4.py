@@ -190,6 +190,8 @@ def _load():
                                 POINTER(c_uint64)] + E, c_int),
         "rt4_progressive_uniforms": ([POINTER(Uniforms), c_uint32, POINTER(Uniforms)], c_int),
         "rt4_render_sections_device": ([c_void_p, POINTER(SectionJob), c_int32, c_int32, c_void_p, c_void_p] + E, c_int),
+        "rt4_debug_verify_div": ([c_void_p, c_float, c_int32, POINTER(c_uint64)] + E, c_int),
+        "rt4_debug_sky_threshold": ([c_void_p, c_float, c_int32, POINTER(c_float)] + E, c_int),
     }
     tolerant = os.environ.get("RT4_AB_TOLERANT") == "1"  # tools/abtest.sh: older builds lack newer exports
     for name, (argtypes, restype) in sig.items():
@@ -210,7 +212,8 @@ EXPORTED = (
     "rt4_scene_builtin rt4_context_create rt4_context_set_scene rt4_context_destroy rt4_render_device rt4_render_host "
     "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt "
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
-    "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device"
+    "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
+    "rt4_debug_verify_div rt4_debug_sky_threshold"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -548,6 +551,20 @@ class Tracer:
         err = _errbuf()
         _check(lib.rt4_debug_verify_sqrt(self._h, ctypes.byref(n), err, len(err)), err)
         return n.value
+
+    def debug_verify_div(self, b: float, full: bool = False) -> int:
+        """Mismatches of the verified-divisor quotient x / b (reduced sweep, or all 2^32 numerators)."""
+        n = c_uint64(0)
+        err = _errbuf()
+        _check(lib.rt4_debug_verify_div(self._h, b, 1 if full else 0, ctypes.byref(n), err, len(err)), err)
+        return n.value
+
+    def debug_sky_threshold(self, ang: float, full: bool = False) -> float:
+        """Smallest float c with acos(c) < ang in the kernel's acos (NaN: none)."""
+        c = c_float(0.0)
+        err = _errbuf()
+        _check(lib.rt4_debug_sky_threshold(self._h, ang, 1 if full else 0, ctypes.byref(c), err, len(err)), err)
+        return c.value
 
     def debug_find_intersection(self, rays):
         import numpy as np

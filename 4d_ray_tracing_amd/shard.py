@@ -1,11 +1,14 @@
 """Pixel-band sharding of one frame over the GPUs of a node.
 
 Every pixel is independent (the RNG depends only on the pixel's scr_coord bits, the seed and its own
-call index: shader.frag:104-108), so a frame splits into disjoint pixel sets with no exchange during
-rendering. Rows are dealt out in bands of `band` rows, round-robin over ranks, so each rank gets the
-same mix of cheap sky rows and expensive object rows. Each rank renders its bands into a contiguous
-buffer (rt4_region band layout, include/rt4.h); one gather to the root and a device-side
-un-permute assemble the image. The assembled image is bit-identical to a 1-GPU render.
+call index: shader.frag:104-108; the whole texture is one draw: src/windows/windows.cpp:45), so a
+frame splits into disjoint pixel sets with no exchange during rendering. Rows are dealt out in bands
+of `band` rows, round-robin over ranks, so each rank gets the same mix of cheap sky rows and
+expensive object rows. Any frame height splits over any number of ranks: the last band of the frame
+may be short, ranks may own one band more than others (or none), and the gather pads every shard to
+the largest one. Each rank renders its bands into a contiguous buffer (rt4_region band layout,
+include/rt4.h); one gather to the root and one device-side row index assemble the image, which is
+bit-identical to a 1-GPU render.
 """
 from __future__ import annotations
 
@@ -15,19 +18,42 @@ from dataclasses import dataclass
 @dataclass(frozen=True)
 class BandPlan:
     width: int
-    rows_per_rank: int
+    height: int  # rows of the whole frame
     world: int
     band: int
 
     @property
-    def height(self) -> int:
-        return self.rows_per_rank * self.world
+    def n_bands(self) -> int:
+        return -(-self.height // self.band)
+
+    def bands(self, rank: int) -> int:
+        """Bands owned by `rank`: r, r + world, r + 2 world, ... below n_bands."""
+        nb = self.n_bands
+        return 0 if rank >= nb else (nb - rank + self.world - 1) // self.world
+
+    def rows(self, rank: int) -> int:
+        """Image rows owned by `rank` (its region height)."""
+        k = self.bands(rank)
+        if k == 0:
+            return 0
+        short = self.n_bands * self.band - self.height  # the frame's last band is this many rows short
+        return k * self.band - (short if (self.n_bands - 1) % self.world == rank else 0)
+
+    @property
+    def rows_max(self) -> int:
+        """Rows of the largest shard: every rank's buffer (and the gather) has this many rows."""
+        return max(1, max(self.rows(r) for r in range(self.world)))
+
+    # weak-scaling plans were sized by rows per rank; kept for callers that think in shards
+    @property
+    def rows_per_rank(self) -> int:
+        return self.rows_max
 
     def region_args(self, rank: int) -> dict:
         """Keyword arguments of rt4.region() for `rank` (local row i -> image row, include/rt4.h)."""
         if self.world == 1:
-            return dict(w=self.width, h=self.rows_per_rank, x0=0, y0=0, band_rows=0, band_step=0)
-        return dict(w=self.width, h=self.rows_per_rank, x0=0, y0=rank * self.band, band_rows=self.band,
+            return dict(w=self.width, h=self.height, x0=0, y0=0, band_rows=0, band_step=0)
+        return dict(w=self.width, h=self.rows(rank), x0=0, y0=rank * self.band, band_rows=self.band,
                     band_step=self.band * self.world)
 
     def image_row(self, rank: int, i: int) -> int:
@@ -35,34 +61,58 @@ class BandPlan:
             return i
         return (i // self.band) * self.band * self.world + rank * self.band + (i % self.band)
 
+    def owner(self, y: int) -> tuple[int, int]:
+        """(rank, local row) of image row y."""
+        b = y // self.band
+        return b % self.world, (b // self.world) * self.band + y % self.band
 
-def make_plan(width: int, rows_per_rank: int, world: int, band: int = 8) -> BandPlan:
-    if world < 1 or rows_per_rank < 1 or width < 1:
-        raise ValueError("width, rows_per_rank and world must be positive")
-    if world > 1 and rows_per_rank % band:
-        raise ValueError(f"rows_per_rank ({rows_per_rank}) must be a multiple of band ({band})")
-    return BandPlan(width, rows_per_rank, world, band)
+    def gather_index(self):
+        """numpy int64 (height,): image row y -> row of the flattened (world * rows_max) gather."""
+        import numpy as np
+
+        y = np.arange(self.height, dtype=np.int64)
+        b = y // self.band
+        return (b % self.world) * self.rows_max + (b // self.world) * self.band + y % self.band
+
+
+def make_plan(width: int, height: int, world: int, band: int = 8) -> BandPlan:
+    """Plan for a width x height frame over `world` ranks in bands of `band` rows. Any height >= 1
+    works; a rank gets no rows when world exceeds the band count."""
+    if world < 1 or height < 1 or width < 1 or band < 1:
+        raise ValueError("width, height, world and band must be positive")
+    return BandPlan(width, height, world, band)
+
+
+def weak_plan(width: int, rows_per_rank: int, world: int, band: int = 8) -> BandPlan:
+    """Weak scaling: a frame of rows_per_rank * world rows, every rank the same number of rows when
+    rows_per_rank is a multiple of band (otherwise the round-robin deal differs by at most one band)."""
+    return make_plan(width, rows_per_rank * world, world, band)
 
 
 def unpermute(gathered, plan: BandPlan):
-    """(world, rows_per_rank, W, 4) gathered shards -> (height, W, 4) image (torch or numpy)."""
+    """(world, rows_max, W, C) gathered shards -> (height, W, C) image (torch or numpy): one row gather."""
     if plan.world == 1:
-        return gathered[0]
-    nb = plan.rows_per_rank // plan.band
-    x = gathered.reshape(plan.world, nb, plan.band, plan.width, 4)
-    if hasattr(x, "permute"):  # torch: one device copy
-        return x.permute(1, 0, 2, 3, 4).reshape(plan.height, plan.width, 4)
-    return x.transpose(1, 0, 2, 3, 4).reshape(plan.height, plan.width, 4)
+        return gathered[0][: plan.height]
+    flat = gathered.reshape((plan.world * plan.rows_max,) + tuple(gathered.shape[2:]))
+    idx = plan.gather_index()
+    if hasattr(flat, "index_select"):  # torch: one device copy
+        import torch
+
+        return flat.index_select(0, torch.from_numpy(idx).to(flat.device))
+    return flat[idx]
 
 
 def gather_frame(local, plan: BandPlan, rank: int, group=None):
-    """Gathers every rank's shard to rank 0 (one collective; RCCL over xGMI with the nccl backend)
-    and returns the assembled image on rank 0, None elsewhere."""
+    """Gathers every rank's shard (rows_max rows each; rows past the rank's own are padding) to rank 0
+    in one collective (RCCL over xGMI with the nccl backend) and returns the assembled image on rank
+    0, None elsewhere."""
     import torch
     import torch.distributed as dist
 
     if plan.world == 1:
         return local
+    if local.shape[0] != plan.rows_max:
+        raise ValueError(f"shard has {local.shape[0]} rows, the plan gathers {plan.rows_max}")
     bufs = [torch.empty_like(local) for _ in range(plan.world)] if rank == 0 else None
     dist.gather(local, gather_list=bufs, dst=0, group=group)
     if rank != 0:

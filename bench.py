@@ -1,25 +1,47 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json metric: ray-bounce intersections/s at 1080p x 16 spp x 8 bounces.
 
-Workload (BASELINE.json configs[1]): the sphere+plane+sun scene
-(scenes/Шар, плоскость и светилник.frag), 1920x1080 pixels per GPU, 16 samples, 8 reflections,
+Workload (BASELINE.json configs[1], SURVEY.md §8(d) config 2, the default): the sphere+plane+sun
+scene (scenes/Шар, плоскость и светилник.frag), 1920x1080 pixels per GPU, 16 samples, 8 reflections,
 seed 12345, default camera, old_frame = 0, part = 1. One "step" = one frame = one launch of the trace
 kernel over the rank's pixels. The unit is one find_intersection() call (shader.frag:475), counted
-on the device by the kernel itself.
+on the device by the kernel itself. `value` is the whole job's units / time (all ranks);
+`value_per_gpu` divides by the GPU count.
 
-Multi-GPU (torchrun): weak scaling — each rank renders 1920x1080 pixels of a 1920x(1080*N) frame,
-dealt in 8-row bands round-robin (4d_ray_tracing_amd/shard.py). The frame is assembled on rank 0 by
-ONE RCCL gather after the K frames, inside the timed region (accumulate locally,
-gather once); --gather every gathers after every frame instead.
+--config picks another BASELINE config (the other fields default to it):
+  2  sphere, 1920x1080 per GPU, 16 spp, 8 bounces, fp32 frame              (weak scaling)
+  3  hypercube, same shape                                                 (weak scaling)
+  4  tiger_two_mirrors, one 3840x2160 frame, 64 spp, 12 bounces            (strong: the frame is split)
+  5  all_primitives, one 3840x2160 frame, 16 spp per progressive frame (part = 1/n, seed_n), 8 bounces,
+     fp16 accumulator; --steps 256 (+ warmup) reaches 4096 spp            (strong)
 
-Prints ONE JSON line on rank 0 with `roofline` (fp32 VALU: oracle-counted fp32 ops per unit x units
-per launch / average kernel time, vs the 157.3 TFLOP/s gfx950 vector peak) and `cpu_baseline`
-(the scalar C++ oracle on this host's cores, on a bounded row sample of the same frame).
+Multi-GPU. `python bench.py --gpus N` starts N ranks itself (torch.distributed.run on 127.0.0.1, one
+process per GPU, before anything touches a GPU) unless it already runs under a launcher
+(WORLD_SIZE set). Pixel bands of 8 rows are dealt round-robin over the ranks
+(4d_ray_tracing_amd/shard.py; any frame height, ragged last band); RCCL gathers the padded shards to
+rank 0, which un-permutes them on the device.
+  weak   (configs 2, 3): every rank renders width x height pixels of a width x (height*N) frame; ONE
+         gather after the K frames, inside the timed region; --gather every: per frame.
+  strong (configs 4, 5, or --strong): the width x height frame is split over the N ranks; config 4
+         gathers every frame (each frame is a finished image), config 5 once after the progressive
+         frames. Rank 0 first renders the whole frame alone (the T1 leg, same steps) and the line
+         reports efficiency = T1 / (N * T_N), both including what the N-rank run does per step.
+
+The JSON line carries `roofline` (fp32 VALU: oracle-counted fp32 ops per unit x units per launch /
+average kernel time from HIP events on the launch stream, vs the 157.3 TFLOP/s gfx950 vector peak;
+`frac_executed` drops the Newton-loop ops the sampler table replaces), `setup_ms` (context + sampler
+table, scene upload + verification) and `cpu_baseline` (the scalar C++ oracle on this job's host
+CPUs, on a bounded row sample of the same frame). `dtype` is the arithmetic type (fp32 in every
+frame format: the blend is fp32, rt4.h rt4_frame_format); `accumulator` is the frame's storage type.
 """
 import argparse
+import glob
 import importlib
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,49 +51,99 @@ sys.path.insert(0, ROOT)
 PEAK_FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
 METRIC = "ray-bounce intersections/s per GPU at 1080p·16spp·8bounce; %VALU roofline"
 
+CONFIGS = {  # BASELINE.json configs[1..4]
+    2: dict(scene="sphere", width=1920, height=1080, spp=16, bounces=8, format="f32", mode="weak", progressive=False),
+    3: dict(scene="hypercube", width=1920, height=1080, spp=16, bounces=8, format="f32", mode="weak", progressive=False),
+    4: dict(scene="tiger_two_mirrors", width=3840, height=2160, spp=64, bounces=12, format="f32", mode="strong",
+            progressive=False),
+    5: dict(scene="all_primitives", width=3840, height=2160, spp=16, bounces=8, format="f16", mode="strong",
+            progressive=True),
+}
 
-def parse_args():
+
+def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--scene", default="sphere")
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080, help="rows per GPU")
-    p.add_argument("--spp", type=int, default=16)
-    p.add_argument("--bounces", type=int, default=8)
+    p.add_argument("--config", type=int, choices=sorted(CONFIGS), default=2)
+    p.add_argument("--scene")
+    p.add_argument("--width", type=int)
+    p.add_argument("--height", type=int, help="weak: rows per GPU; strong: rows of the frame")
+    p.add_argument("--spp", type=int)
+    p.add_argument("--bounces", type=int)
     p.add_argument("--seed", type=int, default=12345)
+    p.add_argument("--format", choices=["f32", "f16", "rgba8"], help="frame format (rt4_frame_format)")
+    g = p.add_mutually_exclusive_group()
+    g.add_argument("--strong", dest="mode", action="store_const", const="strong", help="split one fixed frame")
+    g.add_argument("--weak", dest="mode", action="store_const", const="weak", help="fixed pixels per GPU")
+    p.add_argument("--progressive", action="store_true", default=None, help="part = 1/n, seed_n per step")
+    p.add_argument("--gather", choices=["final", "every"], help="N > 1: RCCL gather once after the frames or per frame")
+    p.add_argument("--no-t1", action="store_true", help="strong, N > 1: skip rank 0's whole-frame leg")
     p.add_argument("--no-lut", action="store_true", help="disable the w_by_volume table (inline Newton loop)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--format", choices=["f32", "f16", "rgba8"], default="f32", help="frame format (rt4_frame_format)")
-    p.add_argument("--gather", choices=["final", "every"], default="final",
-                   help="N > 1: one RCCL gather after the timed frames (default) or one per frame")
-    return p.parse_args()
+    p.add_argument("--no-ops", action="store_true", help="skip the oracle op count (profiling passes)")
+    a = p.parse_args(argv)
+    c = CONFIGS[a.config]
+    for k in ("scene", "width", "height", "spp", "bounces", "format", "mode", "progressive"):
+        if getattr(a, k, None) is None:
+            setattr(a, k, c[k])
+    if a.gather is None:
+        a.gather = "final" if (a.mode == "weak" or a.progressive) else "every"
+    return a
 
 
-def cpu_threads():
-    for k in ("OMP_NUM_THREADS", "RT4_CPU_THREADS"):
-        if os.environ.get(k, "").isdigit():
-            return max(1, int(os.environ[k]))
-    return max(1, min(16, os.cpu_count() or 1))
+# ------------------------------------------------------------------------------------------ host CPUs
+def host_cpus():
+    """CPUs this job may use: the affinity set, capped by the cgroup CPU quota and by the harness's
+    per-GPU share (OMP_NUM_THREADS, 16 on the GPU box, where nproc shows the whole machine)."""
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    if quota:
+        usable = min(usable, max(1, math.floor(quota)))
+    share = os.environ.get("RT4_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    threads = min(usable, int(share)) if share and share.isdigit() and int(share) > 0 else usable
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": max(1, threads), "nproc": nproc, "usable": usable, "cgroup_quota": quota,
+            "share_env": share, "model": model}
 
 
-def cpu_baseline(rt4, scene, u, width, height, target_s):
-    """Oracle (scalar C++ restatement) on rows y = y0 + k*step of the same frame, all host threads."""
+def row_region(rt4, width, height, rows_wanted, y0_hint=3):
+    step = max(1, height // max(1, rows_wanted))
+    y0 = y0_hint % step
+    return rt4.region(width, len(range(y0, height, step)), y0=y0, band_rows=1, band_step=step), step
+
+
+def cpu_baseline(rt4, scene, u, width, height, target_s, cpus):
+    """Oracle (scalar C++ restatement) on rows y = y0 + k*step of the same frame, on this job's CPUs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib  # test infrastructure: only the cpu_baseline leg loads it
+    import oracle_lib  # test infrastructure: only the cpu_baseline / op-count legs load it
 
-    threads = cpu_threads()
-    # probe: two rows on one thread each -> per-row cost; then size the sample for ~target_s
-    probe = rt4.region(width, 2, y0=height // 3, band_rows=1, band_step=height // 3)
+    threads = cpus["threads"]
+    # probe: two rows on two threads ~ one row's time; then size the sample for ~target_s
+    probe = rt4.region(width, 2, y0=height // 3, band_rows=1, band_step=max(1, height // 3))
     t0 = time.perf_counter()
     oracle_lib.render(scene.desc, u, probe, threads=2)
-    per_row = max((time.perf_counter() - t0) / 1.0, 1e-6)  # 2 rows on 2 threads ~ one row's time
-    rows_wanted = max(threads, int(target_s * threads / per_row))
-    step = max(1, height // rows_wanted)
-    y0 = 3 % step
-    reg = rt4.region(width, len(range(y0, height, step)), y0=y0, band_rows=1, band_step=step)
+    per_row = max(time.perf_counter() - t0, 1e-6)
+    reg, step = row_region(rt4, width, height, int(target_s * threads / per_row))
     n, dt, reps = 0, 0.0, 0
     while dt < target_s and reps < 100:  # a whole frame can take less than the target: repeat it
         t0 = time.perf_counter()
@@ -81,37 +153,59 @@ def cpu_baseline(rt4, scene, u, width, height, target_s):
         reps += 1
     what = "the whole frame" if step == 1 else f"every {step}th row ({reg.h} of {height} rows)"
     return {"value": n / dt, "unit": "ray-bounce intersections/s", "cores": threads, "kind": "port",
+            "nproc": cpus["nproc"], "cpu_model": cpus["model"], "cpus_usable": cpus["usable"],
             "sample": f"{what} x {width} px, {u.samples} spp, {u.reflections_amount} bounces, rendered {reps}x: "
-                      f"{n} intersections in {dt:.1f} s; oracle/rt4_oracle.cpp (-O3, scalar) on {threads} host threads"}
+                      f"{n} intersections in {dt:.1f} s; oracle/rt4_oracle.cpp (-O3, scalar) on {threads} threads "
+                      f"(this GPU's CPU share; nproc {cpus['nproc']}, {cpus['model']})"}
 
 
-def ops_per_unit(rt4, scene, u, width, height):
-    """Algorithmic fp32 ops per find_intersection (+ its shading), counted by the oracle on every 64th row."""
+def ops_per_unit(rt4, scene, u, width, height, threads):
+    """Algorithmic fp32 ops per find_intersection (+ its shading), counted by the oracle on ~16 rows
+    of the same frame: (all ops, ops without the Newton loop the sampler table replaces, units)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
-    reg = rt4.region(width, len(range(7, height, 64)), y0=7, band_rows=1, band_step=64)
-    _, n, ops, _ = oracle_lib.render(scene.desc, u, reg, threads=cpu_threads(), count_ops=True)
-    return ops / max(n, 1), n
+    reg, _ = row_region(rt4, width, height, 16, y0_hint=7)
+    n, ops, sampler_ops = oracle_lib.count_ops(scene.desc, u, reg, threads=threads)
+    n = max(n, 1)
+    return ops / n, (ops - sampler_ops) / n, n
 
 
 def pmc_traffic(config):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of the same workload
-    (profiles/pmc_<scene>.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config['scene']}.json")
-    if not os.path.exists(path):
-        return None, None
-    d = json.load(open(path))
-    keys = ("width", "height_per_gpu", "spp", "bounces", "seed", "sampler_lut")
-    pc = dict(d.get("config", {}))
-    pc.setdefault("frame_format", "f32")  # profiles before frame formats existed were float4
-    if any(pc.get(k) != config[k] for k in keys + ("frame_format",)):
-        return None, None
-    return d["derived"].get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same workload and kernel
+    version (profiles/**/pmc_*.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    keys = ("scene", "width", "height_per_gpu", "spp", "bounces", "seed", "sampler_lut", "frame_format",
+            "kernel_version", "progressive")
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_*.json"), recursive=True)):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        pc = d.get("config", {})
+        if all(pc.get(k) == config.get(k) for k in keys) and d.get("derived", {}).get("hbm_bytes_per_launch"):
+            return d["derived"]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+# ------------------------------------------------------------------------------------------ launcher
+def spawn_ranks(args):
+    """`--gpus N` outside a launcher: N fresh processes via torch.distributed.run (this process has
+    not touched a GPU), then exit with their status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -125,30 +219,78 @@ def main():
     rt4 = importlib.import_module("4d_ray_tracing_amd")
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
 
-    plan = shard.make_plan(args.width, args.height, world, band=8)
+    strong = args.mode == "strong"
+    plan = shard.make_plan(args.width, args.height, world) if strong else shard.weak_plan(args.width, args.height, world)
     scene = rt4.Scene.named(args.scene)
     flags = 0 if args.no_lut else rt4.FLAG_SAMPLER_LUT
-    tracer = rt4.Tracer(device=local_rank, flags=flags, scene=scene)
-    u = rt4.make_uniforms(plan.width, plan.height, samples=args.spp, reflections=args.bounces, seed=args.seed)
-    reg = rt4.region(**plan.region_args(rank))
+
+    # setup: context (+ sampler table build) and scene upload (+ divisor / threshold verification)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tracer = rt4.Tracer(device=local_rank, flags=flags)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    tracer.set_scene(scene)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    tracer.set_scene(scene)  # the same scene again: served from the verification cache
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    setup = {"context_ms": (t1 - t0) * 1e3, "set_scene_ms": (t2 - t1) * 1e3, "set_scene_repeat_ms": (t3 - t2) * 1e3}
+
+    base = rt4.make_uniforms(plan.width, plan.height, samples=args.spp, reflections=args.bounces, seed=args.seed)
+    frame_no = [0]
+
+    def uniforms():
+        if not args.progressive:
+            return base
+        frame_no[0] += 1
+        return rt4.progressive_uniforms(base, frame_no[0])
 
     fmt = {"f32": rt4.FRAME_RGBA32F, "f16": rt4.FRAME_RGBA16F, "rgba8": rt4.FRAME_RGBA8}[args.format]
     tdt = {"f32": torch.float32, "f16": torch.float16, "rgba8": torch.uint8}[args.format]
-    frame = torch.zeros((plan.rows_per_rank, plan.width, 4), dtype=tdt, device=dev)
-    counter = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    # ---- T1 leg (strong, N > 1): rank 0 renders the whole frame alone, same warmup/steps
+    t1_ms = None
+    if strong and world > 1 and not args.no_t1:
+        dist.barrier()
+        if rank == 0:
+            full = torch.zeros((plan.height, plan.width, 4), dtype=tdt, device=dev)
+            reg_full = rt4.region(plan.width, plan.height)
+            for _ in range(args.warmup):
+                tracer.render_device_ex(uniforms(), reg_full, full.data_ptr(), fmt, plan.width, 0, sptr)
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            for _ in range(args.steps):
+                tracer.render_device_ex(uniforms(), reg_full, full.data_ptr(), fmt, plan.width, 0, sptr)
+            torch.cuda.synchronize()
+            t1_ms = (time.perf_counter() - ta) / args.steps * 1e3
+            del full
+            frame_no[0] = 0
+        dist.barrier()
+
+    reg = rt4.region(**plan.region_args(rank))
+    frame = torch.zeros((plan.rows_max, plan.width, 4), dtype=tdt, device=dev)  # padded shard (gather)
+    gathers = []
 
     def render():
-        tracer.render_device_ex(u, reg, frame.data_ptr(), fmt, plan.width, counter.data_ptr(), sptr)
+        tracer.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, counter.data_ptr(), sptr)
 
-    def step():
-        render()
-        if world > 1:
-            shard.gather_frame(frame, plan, rank)
+    def gather():
+        g0 = torch.cuda.Event(enable_timing=True)
+        g1 = torch.cuda.Event(enable_timing=True)
+        g0.record(stream)
+        shard.gather_frame(frame, plan, rank)  # the frame assembled (un-permuted) on rank 0
+        g1.record(stream)
+        gathers.append((g0, g1))
 
     for _ in range(args.warmup):
-        step()
+        render()
+        if world > 1 and args.gather == "every":
+            shard.gather_frame(frame, plan, rank)
     torch.cuda.synchronize()
     counter.zero_()
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -162,38 +304,44 @@ def main():
         render()
         k_end[i].record(stream)
         if world > 1 and args.gather == "every":
-            shard.gather_frame(frame, plan, rank)
-    g0 = torch.cuda.Event(enable_timing=True)
-    g1 = torch.cuda.Event(enable_timing=True)
-    g0.record(stream)
+            gather()
     if world > 1 and args.gather == "final":
-        shard.gather_frame(frame, plan, rank)  # the frame assembled on rank 0
-    g1.record(stream)
+        gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / args.steps
+    gather_ms = sum(a.elapsed_time(b) for a, b in gathers) / len(gathers) if gathers else 0.0
 
-    gather_ms = g0.elapsed_time(g1)
     n_local = int(counter.item())
-    stats = torch.tensor([elapsed, float(n_local), kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        t_max = stats[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        n_sum = stats[1:2].clone()
+        st = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        n_sum = torch.tensor([n_local], dtype=torch.int64, device=dev)
         dist.all_reduce(n_sum, op=dist.ReduceOp.SUM)
-        k_max = stats[2:3].clone()
-        dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
-        elapsed, n_total, kernel_ms = float(t_max.item()), float(n_sum.item()), float(k_max.item())
+        elapsed, kernel_ms, gather_ms = (float(x) for x in st.tolist())
+        n_total = int(n_sum.item())
     else:
-        n_total = float(n_local)
+        n_total = n_local
 
     if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
         value = n_total / elapsed
-        units_per_launch = n_local / args.steps
-        opu, _ = ops_per_unit(rt4, scene, u, plan.width, plan.height)
-        achieved = opu * units_per_launch / (kernel_ms * 1e-3) / 1e12
+        units_per_launch = n_total / world / args.steps  # per rank (kernel_ms is the max over ranks)
+        cpus = host_cpus()
+        version = rt4.lib.rt4_build_info().decode().split()[2]
+        config = {
+            "workload": (f"config {args.config}: {args.scene} scene, frame {plan.width}x{plan.height}"
+                         + (f" ({plan.width}x{plan.rows_max} px per GPU)" if world > 1 else "")
+                         + f", {args.spp} spp{' per progressive frame' if args.progressive else ''}, "
+                           f"{args.bounces} bounces, seed {args.seed}, {args.format} frame"),
+            "config": args.config, "scene": args.scene, "width": plan.width,
+            "height": plan.height, "height_per_gpu": plan.rows_max, "spp": args.spp, "bounces": args.bounces,
+            "seed": args.seed, "sampler_lut": not args.no_lut, "frame_format": args.format,
+            "progressive": bool(args.progressive), "kernel_version": version,
+            "parallelism": f"pixel-bands x{world}" + (f" + RCCL gather ({args.gather})" if world > 1 else ""),
+        }
         line = {
             "metric": METRIC,
             "value": value,
@@ -201,43 +349,49 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.mode,
             "vs_baseline": None,
             "dtype": "fp32",
+            "accumulator": args.format,
             "data": "synthetic (fixed-seed procedural scene, no dataset)",
-            "config": {
-                "workload": f"{args.scene} scene, {plan.width}x{plan.rows_per_rank} px per GPU "
-                            f"(frame {plan.width}x{plan.height}), {args.spp} spp, {args.bounces} bounces, seed {args.seed}",
-                "scene": args.scene, "width": plan.width, "height_per_gpu": plan.rows_per_rank,
-                "spp": args.spp, "bounces": args.bounces, "seed": args.seed,
-                "sampler_lut": not args.no_lut,
-                "parallelism": f"pixel-bands x{world}" + (f" + RCCL gather ({args.gather})" if world > 1 else ""),
-                "frame_format": args.format,
-            },
-            "gather_ms": gather_ms if world > 1 else 0.0,
+            "config": config,
+            "value_per_gpu": value / world,
+            "gather_ms": gather_ms,
             "intersections_per_step": n_total / args.steps,
             "nominal_bound_per_step": plan.width * plan.height * args.spp * (args.bounces + 1),
             "kernel_ms": kernel_ms,
-            "roofline": {
+            "setup_ms": setup,
+        }
+        if strong:
+            line["t1_ms"] = t1_ms if world > 1 else ms_per_step
+            line["efficiency"] = (line["t1_ms"] / (world * ms_per_step)) if line["t1_ms"] else None
+        if not args.no_ops:
+            opu, opu_exec, _ = ops_per_unit(rt4, scene, base, plan.width, plan.height, cpus["threads"])
+            achieved = opu * units_per_launch / (kernel_ms * 1e-3) / 1e12
+            achieved_exec = (opu if args.no_lut else opu_exec) * units_per_launch / (kernel_ms * 1e-3) / 1e12
+            traffic, src = pmc_traffic(config)
+            line["roofline"] = {
                 "bound": "valu",
                 "achieved": achieved,
                 "peak": PEAK_FP32_VALU_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_VALU_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
                 "ops_per_unit": opu,
-                "note": "fp32 ops (fma=2) per find_intersection+shading counted by the oracle; see DESIGN.md §5",
-            },
-        }
-        traffic, src = pmc_traffic(line["config"])
-        line["roofline"]["traffic"] = traffic
-        if src:
-            line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per launch)"
-            line["roofline"]["algorithmic_bytes_per_launch"] = plan.width * plan.rows_per_rank * 32
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(rt4, scene, u, plan.width, plan.rows_per_rank, args.cpu_seconds)
+                "ops_per_unit_executed": opu if args.no_lut else opu_exec,
+                "frac_executed": achieved_exec / PEAK_FP32_VALU_TFLOPS,
+                "units_per_launch": units_per_launch,
+                "algorithmic_bytes_per_launch": reg.w * reg.h * 2 * rt4.frame_format_bytes(fmt),  # old_frame in, new out
+                "note": "fp32 ops (fma=2) per find_intersection+shading counted by the oracle on a row sample of "
+                        "the frame; executed = without the w_by_volume Newton ops the sampler table replaces; "
+                        "see DESIGN.md §5",
+            }
+            if src:
+                line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per launch)"
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(rt4, scene, base, plan.width, plan.rows_max, args.cpu_seconds, cpus)
         print(json.dumps(line), flush=True)
     tracer.close()
     if world > 1:

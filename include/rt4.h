@@ -297,6 +297,10 @@ typedef struct rt4_context rt4_context;
 #define RT4_FLAG_GENERIC_KERNEL 0x2u
 
 int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err, size_t errlen);
+/* Uploads a scene (the reference recompiles the shader: src/main.cpp:25-39). Waits for the
+ * context's launches still in flight on any stream before it replaces the device copy, so a frame
+ * issued earlier renders the previous scene. Scene constants are verified on the device once per
+ * process (cached by bit pattern), so setting a scene seen before costs only the upload. */
 int rt4_context_set_scene(rt4_context* ctx, const rt4_scene_desc* scene, char* err, size_t errlen);
 void rt4_context_destroy(rt4_context* ctx);
 
@@ -392,6 +396,15 @@ int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out,
 /* Counts the 32-bit patterns x for which the kernel's sqrt (fast path without input scaling) differs
  * from the IEEE square root; 0 expected. Exhaustive over all 2^32 inputs on the device (~10 ms). */
 int rt4_debug_verify_sqrt(rt4_context* ctx, uint64_t* mismatches, char* err, size_t errlen);
+
+/* The scene-constant checks of rt4_context_set_scene, alone (synchronous). verify_div: mismatches of
+ * the verified-divisor quotient against x / b over the reduced sweep (full = 0: positive numerators,
+ * edge exponents + three of the middle band) or over all 2^32 numerators (full = 1);
+ * set_scene enables the fast quotient iff the reduced count is 0. sky_threshold: the smallest float c
+ * with acos(c) < ang in the kernel's acos (NaN: none), over c in (0.5, 1] for ang <= 1 (full = 0) or
+ * over all 2^32 patterns (full = 1). */
+int rt4_debug_verify_div(rt4_context* ctx, float b, int32_t full, uint64_t* mismatches, char* err, size_t errlen);
+int rt4_debug_sky_threshold(rt4_context* ctx, float ang, int32_t full, float* c_min, char* err, size_t errlen);
 
 /* Trace kernel selected for the context's scene: 0xFFFFFFFF = the generic find_intersection
  * (any group list); otherwise the K_* group bits (low byte: 1 spaces, 2 spheres, 4 cylinders,

@@ -40,6 +40,9 @@ namespace {
 
 // ---------------------------------------------------------------- op-counting fp32 scalar
 thread_local uint64_t g_ops = 0;
+// ops spent inside w_by_volume's Newton loop (rand_drct): the sampler table (RT4_FLAG_SAMPLER_LUT)
+// replaces exactly these with one load, so "executed" counts for the LUT kernel drop them
+thread_local uint64_t g_sampler_ops = 0;
 
 struct CF {
   float v;
@@ -229,7 +232,9 @@ template <class F> F w_by_volume(F v, int* iters) {  // :141-150
   return new_w;
 }
 template <class F> V4<F> rand_drct(Rng& rng) {  // :153-158, cyl_vec_to_vec :128-130
+  const uint64_t ops0 = g_ops;
   F w = w_by_volume(F(rng.rand()), nullptr);
+  g_sampler_ops += g_ops - ops0;
   F r = sqrt_(F(1.0f) - w * w);
   F z = (F(rng.rand()) * F(2.0f) - F(1.0f)) * r;
   F rr = sqrt_(r * r - z * z);
@@ -535,15 +540,23 @@ inline int region_row(const rt4_region& r, int i) {
 
 template <class F>
 void render_rows(const rt4_scene_desc& s, const rt4_uniforms& u, const rt4_region& reg, float* rgba, int64_t stride,
-                 int threads, uint64_t* n_inter, uint64_t* ops, uint32_t* pixel_counts, int32_t fmt = RT4_FRAME_RGBA32F) {
+                 int threads, uint64_t* n_inter, uint64_t* ops, uint32_t* pixel_counts, int32_t fmt = RT4_FRAME_RGBA32F,
+                 uint64_t* sampler_ops = nullptr) {
   const int64_t px_bytes = fmt == RT4_FRAME_RGBA16F ? 8 : (fmt == RT4_FRAME_RGBA8 ? 4 : 16);
-  std::atomic<uint64_t> total_inter{0}, total_ops{0};
+  std::atomic<uint64_t> total_inter{0}, total_ops{0}, total_sampler{0};
+  // work items: 64-pixel pieces of rows, interleaved over the threads (balances sky vs object rows, and
+  // keeps every thread busy when the region has fewer rows than threads)
+  constexpr int PIECE = 64;
+  const int64_t pieces = (reg.w + PIECE - 1) / PIECE, items = pieces * reg.h;
   auto worker = [&](int t) {
     uint64_t my_inter = 0;
     g_ops = 0;
-    for (int i = t; i < reg.h; i += threads) {  // interleaved rows: balances sky vs object rows
+    g_sampler_ops = 0;
+    for (int64_t it = t; it < items; it += threads) {
+      const int i = static_cast<int>(it / pieces);
       const int y = region_row(reg, i);
-      for (int j = 0; j < reg.w; j++) {
+      const int j0 = static_cast<int>(it % pieces) * PIECE, j1 = std::min(reg.w, j0 + PIECE);
+      for (int j = j0; j < j1; j++) {
         uint64_t before = my_inter;
         render_pixel<F>(s, u, reg.x0 + j, y,
                         reinterpret_cast<float*>(reinterpret_cast<char*>(rgba) + px_bytes * (static_cast<int64_t>(i) * stride + j)),
@@ -553,6 +566,7 @@ void render_rows(const rt4_scene_desc& s, const rt4_uniforms& u, const rt4_regio
     }
     total_inter += my_inter;
     total_ops += g_ops;
+    total_sampler += g_sampler_ops;
   };
   if (threads <= 1) {
     worker(0);
@@ -563,6 +577,7 @@ void render_rows(const rt4_scene_desc& s, const rt4_uniforms& u, const rt4_regio
   }
   if (n_inter) *n_inter = total_inter.load();
   if (ops) *ops = total_ops.load();
+  if (sampler_ops) *sampler_ops = total_sampler.load();
 }
 
 }  // namespace
@@ -646,6 +661,20 @@ int oracle_render(const rt4_scene_desc* s, const rt4_uniforms* u, const rt4_regi
     render_rows<CF>(*s, *u, *reg, rgba, row_stride_px, threads, n_intersections, ops, pixel_counts);
   else
     render_rows<float>(*s, *u, *reg, rgba, row_stride_px, threads, n_intersections, nullptr, pixel_counts);
+  return RT4_OK;
+}
+
+// The op-counting render alone: *ops = all fp32 ops (as oracle_render with count_ops), *sampler_ops =
+// the part of them inside w_by_volume (shader.frag:141-150), which the sampler-table kernel replaces
+// by one load. Executed ops per unit with the table = (ops - sampler_ops) / n_intersections.
+int oracle_count_ops(const rt4_scene_desc* s, const rt4_uniforms* u, const rt4_region* reg, float* rgba,
+                     int64_t row_stride_px, int32_t threads, uint64_t* n_intersections, uint64_t* ops,
+                     uint64_t* sampler_ops) {
+  if (!s || !u || !reg || !rgba) return RT4_ERR_ARG;
+  if (reg->w < 0 || reg->h < 0 || row_stride_px < reg->w) return RT4_ERR_ARG;
+  if (threads < 1) threads = 1;
+  render_rows<CF>(*s, *u, *reg, rgba, row_stride_px, threads, n_intersections, ops, nullptr, RT4_FRAME_RGBA32F,
+                  sampler_ops);
   return RT4_OK;
 }
 

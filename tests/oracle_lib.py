@@ -88,6 +88,22 @@ def render(scene_desc, uniforms, reg, frame=None, threads=None, count_ops=False,
     return frame, n.value, ops.value, counts
 
 
+def count_ops(scene_desc, uniforms, reg, threads=None):
+    """Op-counting render of `reg` (oracle_count_ops): (n_intersections, fp32 ops, ops inside the
+    w_by_volume Newton loop, which the sampler-table kernel replaces by one load)."""
+    lib_ = lib()
+    lib_.oracle_count_ops.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, POINTER(c_uint64),
+                                      POINTER(c_uint64), POINTER(c_uint64)]
+    lib_.oracle_count_ops.restype = ctypes.c_int
+    frame = np.zeros((reg.h, reg.w, 4), np.float32)
+    n, ops, sops = c_uint64(), c_uint64(), c_uint64()
+    st = lib_.oracle_count_ops(ctypes.addressof(scene_desc), ctypes.addressof(uniforms), ctypes.addressof(reg),
+                               frame.ctypes.data, reg.w, threads or os.cpu_count() or 1, ctypes.byref(n),
+                               ctypes.byref(ops), ctypes.byref(sops))
+    assert st == 0
+    return n.value, ops.value, sops.value
+
+
 FRAME_DTYPES = {0: np.float32, 1: np.float16, 2: np.uint8}
 
 

@@ -1,4 +1,4 @@
-"""bench.py on the GPU: the one JSON line the driver parses (contract keys, roofline, config 2 shape)."""
+"""bench.py on the GPU: the one JSON line the driver parses (contract keys, roofline, config shapes)."""
 import json
 import os
 import subprocess
@@ -10,20 +10,37 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_json_line():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=110, cwd=ROOT)
+def run_bench(*args, timeout=110):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
-    d = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_json_line():
+    d = run_bench("--steps", "3", "--warmup", "1", "--no-cpu-baseline")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-              "vs_baseline", "dtype", "data", "config", "roofline"):
+              "vs_baseline", "dtype", "data", "config", "roofline", "setup_ms", "value_per_gpu"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["higher_is_better"] is True
-    assert d["config"]["width"] == 1920 and d["config"]["height_per_gpu"] == 1080
-    assert d["config"]["spp"] == 16 and d["config"]["bounces"] == 8 and d["config"]["seed"] == 12345
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    c = d["config"]
+    assert c["width"] == 1920 and c["height_per_gpu"] == 1080 and c["config"] == 2
+    assert c["spp"] == 16 and c["bounces"] == 8 and c["seed"] == 12345
     assert d["intersections_per_step"] == 56746603  # the oracle's count for config 2
-    assert d["value"] > 1e9
+    assert d["value"] > 1e9 and d["value_per_gpu"] == d["value"]
     rf = d["roofline"]
     assert 0 < rf["frac"] < 1 and rf["peak"] == 157.3 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"])
+    assert rf["ops_per_unit_executed"] < rf["ops_per_unit"] and rf["frac_executed"] < rf["frac"]
+    assert d["setup_ms"]["set_scene_repeat_ms"] < d["setup_ms"]["set_scene_ms"] + 1.0
+
+
+def test_bench_strong_config4_one_gpu():
+    """Config 4 in strong mode on one GPU: the whole 3840x2160 frame per step, efficiency 1 by definition."""
+    d = run_bench("--config", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", timeout=115)
+    assert d["scaling"] == "strong" and d["n_gpus"] == 1
+    c = d["config"]
+    assert (c["scene"], c["width"], c["height"], c["spp"], c["bounces"]) == ("tiger_two_mirrors", 3840, 2160, 64, 12)
+    assert d["efficiency"] == pytest.approx(1.0)
+    assert d["intersections_per_step"] <= d["nominal_bound_per_step"]

@@ -217,6 +217,8 @@ def test_launches_on_two_streams_and_a_large_frame(rt4, oracle):
         reg = rt4.region(160, 100)
         s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
         frames = [torch.zeros((100, 160, 4), device="cuda") for _ in range(4)]
+        for st in (s1, s2):  # the zero-fills (current stream) before the side streams' kernels
+            st.wait_stream(torch.cuda.current_stream())
         for q, fr in enumerate(frames):
             st = s1 if q % 2 == 0 else s2
             t.render_device(u, reg, fr.data_ptr(), 160, 0, st.cuda_stream)
@@ -283,6 +285,8 @@ def test_queue_words_across_many_launches(rt4, oracle):
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
         fr = torch.zeros((H, W, 4), device="cuda")
         counts = torch.zeros(150, dtype=torch.int64, device="cuda")
+        for st in streams:  # the zero-fills (current stream) before the side streams' kernels
+            st.wait_stream(torch.cuda.current_stream())
         for q in range(150):
             st = streams[(q // 7) % 2]
             if q % 11 == 5:  # an empty region launches nothing and must not consume a queue word

@@ -359,3 +359,44 @@ def test_golden_images(rt4, name):
     ref = np.load(os.path.join(GOLDEN, f"image_{name}.npy"))
     assert n == meta["intersections"]
     assert_bits(f, ref, f"golden {name}")
+
+
+# ------------------------------------------------------------------- scene-constant verification
+def test_reduced_divisor_sweep_agrees_with_full(tracer, rt4):
+    """rt4_context_set_scene enables the 3-op quotient for a divisor after a REDUCED sweep (positive
+    numerators; exponent fields outside the middle band, plus three fields of it: DESIGN.md §4.5). On
+    every divisor of the seven scenes and on random ones over the whole exponent range it must decide
+    exactly as the sweep over all 2^32 numerators."""
+    divs = set()
+    for name in SCENES:
+        d = rt4.Scene.named(name).desc
+        divs |= {d.spheres[i].r for i in range(d.n_spheres)} | {d.cylinders[i].r for i in range(d.n_cylinders)}
+        for i in range(d.n_unions):
+            divs |= {d.unions[i].cylinder1.r, d.unions[i].cylinder2.r}
+        for i in range(d.n_tigers):
+            t = d.tigers[i]
+            divs |= {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r}
+        divs.add(d.sun.angular_size)
+    rng = np.random.default_rng(11)
+    rand = (rng.uniform(0.5, 1.0, 24) * 2.0 ** rng.integers(-120, 120, 24)).astype(np.float32)
+    divs |= {float(x) for x in rand} | {3.0, 0.1, 1.0, 7.0, 1e-30, 3e30}
+    decided = {True: 0, False: 0}
+    for b in sorted(divs):
+        red, full = tracer.debug_verify_div(b), tracer.debug_verify_div(b, full=True)
+        assert (red == 0) == (full == 0), (b, red, full)
+        assert red <= full
+        decided[full == 0] += 1
+    assert decided[True] > 0 and decided[False] > 0  # both outcomes occur: the check has teeth
+
+
+def test_sky_threshold_sweep_restriction(tracer, rt4):
+    """For sun angular sizes <= 1 set_scene searches the acos threshold over c in (0.5, 1] only. The
+    full 2^32 search at ang = 1 lands above 0.5, which proves that no c <= 0.5 has acos(c) < 1 (and so
+    < any smaller ang); restricted and full searches agree on the scenes' suns and random sizes."""
+    c1 = tracer.debug_sky_threshold(1.0, full=True)
+    assert c1 > 0.5
+    angs = {rt4.Scene.named(n).desc.sun.angular_size for n in SCENES}
+    angs |= {float(x) for x in np.random.default_rng(3).uniform(1e-4, 1.0, 6).astype(np.float32)} | {1.0}
+    for a in sorted(angs):
+        r, f = tracer.debug_sky_threshold(a), tracer.debug_sky_threshold(a, full=True)
+        assert (np.isnan(r) and np.isnan(f)) or np.float32(r).view(np.uint32) == np.float32(f).view(np.uint32), (a, r, f)

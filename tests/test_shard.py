@@ -1,6 +1,9 @@
-"""Pixel-band sharding (4d_ray_tracing_amd/shard.py) on the CPU: gloo process groups of world size 2 and
-3, the CPU oracle as each rank's renderer, one gather to rank 0 -> the assembled frame must equal a
-single full render bit for bit (the RNG depends only on the pixel)."""
+"""Pixel-band sharding (4d_ray_tracing_amd/shard.py) on the CPU: gloo process groups of world size 2,
+3 and 8 on frame heights that do not divide evenly (2160 = the 4K frame of BASELINE configs 4/5,
+1081 = a short last band), the CPU oracle as each rank's renderer, one padded gather to rank 0 ->
+the assembled frame must equal a single full render bit for bit (the RNG depends only on the pixel,
+shader.frag:104-108). The same plan drives librt4.so on the GPU
+(tests/test_gpu_shard.py, bench.py)."""
 import importlib
 import os
 import socket
@@ -23,7 +26,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, scene_name, out_dir):
+def _worker(rank, world, port, scene_name, width, height, out_dir):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -31,12 +34,15 @@ def _worker(rank, world, port, scene_name, out_dir):
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
     import oracle_lib
 
-    plan = shard.make_plan(width=40, rows_per_rank=16, world=world, band=8)
+    plan = shard.make_plan(width, height, world, band=8)
     scene = rt4.Scene.named(scene_name)
-    u = rt4.make_uniforms(plan.width, plan.height, samples=2, reflections=3, seed=31337)
+    u = rt4.make_uniforms(plan.width, plan.height, samples=1, reflections=2, seed=31337)
     reg = rt4.region(**plan.region_args(rank))
-    frame, n, _, _ = oracle_lib.render(scene.desc, u, reg, threads=2)
-    image = shard.gather_frame(torch.from_numpy(frame), plan, rank)
+    local = np.zeros((plan.rows_max, plan.width, 4), np.float32)  # padded shard: rows past reg.h stay 0
+    n = 0
+    if reg.h:
+        _, n, _, _ = oracle_lib.render(scene.desc, u, reg, frame=local, threads=1)
+    image = shard.gather_frame(torch.from_numpy(local), plan, rank)
     total = torch.tensor([n], dtype=torch.int64)
     dist.all_reduce(total)
     if rank == 0:
@@ -45,35 +51,64 @@ def _worker(rank, world, port, scene_name, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_banded_gather_equals_full_frame(tmp_path, world):
+@pytest.mark.parametrize("world,height", [(2, 2160), (3, 1081), (8, 2160), (8, 1081)])
+def test_banded_gather_equals_full_frame(tmp_path, world, height):
     rt4 = importlib.import_module("4d_ray_tracing_amd")
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
     import oracle_lib
 
-    tmp.spawn(_worker, args=(world, _free_port(), "cylinder4d", str(tmp_path)), nprocs=world, join=True)
+    width = 12
+    tmp.spawn(_worker, args=(world, _free_port(), "cylinder4d", width, height, str(tmp_path)), nprocs=world, join=True)
     image = np.load(tmp_path / "image.npy")
     n = int(np.load(tmp_path / "n.npy")[0])
-    plan = shard.make_plan(width=40, rows_per_rank=16, world=world, band=8)
-    u = rt4.make_uniforms(plan.width, plan.height, samples=2, reflections=3, seed=31337)
-    full, n_full, _, _ = oracle_lib.render(rt4.Scene.named("cylinder4d").desc, u, rt4.region(plan.width, plan.height))
+    u = rt4.make_uniforms(width, height, samples=1, reflections=2, seed=31337)
+    full, n_full, _, _ = oracle_lib.render(rt4.Scene.named("cylinder4d").desc, u, rt4.region(width, height), threads=4)
+    assert image.shape == full.shape
     assert n == n_full
     assert np.array_equal(image.view(np.uint32), full.view(np.uint32))
 
 
-def test_plan_rows_partition_the_frame():
+@pytest.mark.parametrize("height", [1, 7, 8, 9, 63, 1080, 1081, 2160, 2161, 4320])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize("band", [1, 8, 16])
+def test_plan_rows_partition_the_frame(height, world, band):
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
-    for world in (1, 2, 4, 8):
-        plan = shard.make_plan(1920, 1080, world)
-        rows = sorted(plan.image_row(r, i) for r in range(world) for i in range(plan.rows_per_rank))
-        assert rows == list(range(plan.height))
-        # the numpy un-permute agrees with image_row()
-        tag = np.zeros((world, plan.rows_per_rank, 1, 4), np.int64)
-        for r in range(world):
-            for i in range(plan.rows_per_rank):
-                tag[r, i] = plan.image_row(r, i)
-        plan1 = shard.BandPlan(1, plan.rows_per_rank, world, plan.band)
-        img = shard.unpermute(tag, plan1)
-        assert (img[:, 0, 0] == np.arange(plan.height)).all()
+    plan = shard.make_plan(1920, height, world, band=band)
+    rows = [plan.rows(r) for r in range(world)]
+    assert sum(rows) == height
+    assert plan.rows_max == max(1, max(rows))
+    # round-robin bands: shares differ by at most one band
+    assert max(rows) - min(rows) <= band
+    owned = sorted(plan.image_row(r, i) for r in range(world) for i in range(rows[r]))
+    assert owned == list(range(height))
+    for r in range(world):
+        for i in range(rows[r]):
+            assert plan.owner(plan.image_row(r, i)) == (r, i)
+    # the row index of the padded gather agrees with image_row(), numpy and torch alike
+    tag = np.full((world, plan.rows_max, 1, 4), -1, np.int64)
+    for r in range(world):
+        for i in range(rows[r]):
+            tag[r, i] = plan.image_row(r, i)
+    img = shard.unpermute(tag, plan)
+    assert (img[:, 0, 0] == np.arange(height)).all()
+    timg = shard.unpermute(torch.from_numpy(tag), plan)
+    assert (timg[:, 0, 0].numpy() == np.arange(height)).all()
+
+
+def test_4k_over_8_ranks_is_balanced():
+    """BASELINE configs 4/5: 3840x2160 over 8 GPUs in 8-row bands -> 270 bands, 6 ranks x 34 + 2 x 33;
+    the largest share is 0.7 % above the mean (the bound on strong-scaling efficiency from the split)."""
+    shard = importlib.import_module("4d_ray_tracing_amd.shard")
+    plan = shard.make_plan(3840, 2160, 8)
+    assert [plan.bands(r) for r in range(8)] == [34] * 6 + [33] * 2
+    assert plan.rows_max == 272
+    assert plan.rows_max / (2160 / 8) < 1.01
+
+
+def test_bad_plans_raise():
+    shard = importlib.import_module("4d_ray_tracing_amd.shard")
+    for args in [(0, 10, 1), (10, 0, 1), (10, 10, 0)]:
+        with pytest.raises(ValueError):
+            shard.make_plan(*args)
     with pytest.raises(ValueError):
-        shard.make_plan(1920, 1081, 2)
+        shard.make_plan(10, 10, 2, band=0)
