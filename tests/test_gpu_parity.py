@@ -380,6 +380,7 @@ def test_reduced_divisor_sweep_agrees_with_full(tracer, rt4):
     rng = np.random.default_rng(11)
     rand = (rng.uniform(0.5, 1.0, 24) * 2.0 ** rng.integers(-120, 120, 24)).astype(np.float32)
     divs |= {float(x) for x in rand} | {3.0, 0.1, 1.0, 7.0, 1e-30, 3e30}
+    divs = {b for b in divs if np.isfinite(b) and b != 0 and np.isfinite(np.float32(1) / np.float32(b))}
     decided = {True: 0, False: 0}
     for b in sorted(divs):
         red, full = tracer.debug_verify_div(b), tracer.debug_verify_div(b, full=True)

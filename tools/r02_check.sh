@@ -5,7 +5,7 @@ set -u -o pipefail
 OUT=gpurun_out/${1:-r02}
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 240 --timeout-method thread \
   > "$OUT/pytest_gpu.log" 2>&1 || { echo "pytest failed"; tail -40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -3 "$OUT/pytest_gpu.log"
 for args in "" "--config 3" "--config 4 --steps 5 --warmup 1" "--config 5 --steps 32 --warmup 1"; do
