@@ -82,6 +82,12 @@ def main():
         m["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         m["hbm_bytes_per_launch"] = m["hbm_read_bytes_corrected"] + m["hbm_write_bytes"]
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        m["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if "TCC_EA0_RDREQ_sum" in c and "TCC_EA0_RDREQ_DRAM_sum" in c:
+        # L2 misses sent to the fabric, and the part of them that reached DRAM (the rest: MALL hits)
+        m["fabric_read_requests"] = c["TCC_EA0_RDREQ_sum"]
+        m["dram_read_share"] = c["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, c["TCC_EA0_RDREQ_sum"])
     out["derived"] = m
     for log in ("trace.log", os.path.join("trace", "..", "bench.log")):
         lp = os.path.join(d, log)
@@ -91,6 +97,8 @@ def main():
                 b = json.loads(lines[-1])
                 out["config"] = b["config"]
                 out["bench"] = {k: b[k] for k in ("value", "kernel_ms", "intersections_per_step")}
+                if out.get("avg_ns"):
+                    out["bench"]["kernel_ms_vs_trace"] = b["kernel_ms"] / (out["avg_ns"] * 1e-6)
                 n = b["intersections_per_step"]
                 if "SQ_INSTS_VALU" in c:
                     m["valu_lane_slots_per_intersection"] = c["SQ_INSTS_VALU"] * 64 / n

@@ -28,4 +28,5 @@ run pmc_cyc --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VA
 run pmc_thr --kernel-trace --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA || true
 run pmc_fetch --kernel-trace --pmc FETCH_SIZE || exit 1
 run pmc_write --kernel-trace --pmc WRITE_SIZE || exit 1
+run pmc_tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum || true
 echo "profile $TAG done"
