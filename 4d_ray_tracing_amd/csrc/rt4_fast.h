@@ -442,7 +442,8 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
 #ifdef RT4_LANESTATS  // diagnostic: pending-loop trips and their active lanes, per block in LDS
       {
         const unsigned long long ex = __builtin_amdgcn_read_exec();
-        if ((threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+        // the pointer is set by the trace kernel only: null in the tile-order and find kernels
+        if (rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
           atomicAdd(rt4_ls_counter + 40, 1ull);
           atomicAdd(rt4_ls_counter + 41, static_cast<unsigned long long>(__popcll(ex)));
         }

@@ -316,7 +316,6 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   }
   const PrimEntry* P = reinterpret_cast<const PrimEntry*>(lds_prims + CELLS4);
 
-  unsigned b_next = 0, b_end = 0;  // wave-uniform: unclaimed part of the current batch
   bool exhausted = false;
   bool active = false, pending = false;
   RngState rng{0u, 0u};
@@ -327,6 +326,20 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   // so the VGPRs go to occupancy instead (6 -> 7 waves/SIMD on the sphere scene).
   __shared__ float4 lds_cold[2 * 256];
   float4* const cold = lds_cold + threadIdx.x;
+  // Per-wave pixel I/O staged in LDS, 64 entries per wave:
+  //   inbox: when the wave claims a 64-pixel batch (one 8x8 tile of one job), all 64 lanes set up the
+  //     batch's pixels at once (scr_coord, RNG base, primary direction: shader.frag:501-505, :515-516);
+  //     an idle lane starts a pixel by reading its entry ({d0}, {RNG base, pack_pixel or ~0 = none}).
+  //   outbox: a lane whose pixel has run all its samples appends {light sum, pack_pixel} to the wave's
+  //     ring; the wave writes the ring out 64 pixels at a time (old_frame read, tone map, blend:
+  //     shader.frag:522-527), so the old_frame load latency and the write arithmetic are paid once per
+  //     64 pixels with every lane busy, instead of per pixel on one or two lanes.
+  __shared__ float4 lds_in_d0[256];
+  __shared__ uint2 lds_in_px[256];
+  __shared__ float4 lds_out[256];
+  const unsigned wbase = threadIdx.x & ~63u;
+  unsigned in_next = 64;  // wave-uniform: next inbox entry to hand out (64: empty)
+  unsigned ring_n = 0;    // wave-uniform: outbox entries waiting to be written
   int s = 0, b = 0;
   uint32_t n_inter = 0;
 
@@ -338,13 +351,64 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;
   RT4_STAMP(t_loop0);
 #endif
-  // writes the finished pixels of the active lanes; one wave-uniform pass per job, so every job's
-  // frame pointer and stride stay scalar (a per-lane select held them in VGPRs: 8 more per lane)
-  auto flush_pixel = [&]() {
-    const float4 lp = cold[256];
-    const int pk = __float_as_int(lp.w);
-    for (int jb = 0; jb < a.n_jobs; jb++)
-      if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
+  // Writes the outbox ring (lane q takes entry q); one wave-uniform pass per job, so every job's frame
+  // pointer and stride stay scalar.
+  auto flush_ring = [&]() {
+    if (lane < ring_n) {
+      const float4 lp = lds_out[wbase + lane];
+      const int pk = __float_as_int(lp.w);
+      for (int jb = 0; jb < a.n_jobs; jb++)
+        if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
+    }
+    ring_n = 0;
+  };
+  // Moves the finished pixels of the pending lanes into the ring (writing the ring out first when they
+  // would not fit).
+  auto retire = [&]() {
+    const unsigned long long pm = __ballot(pending);
+    if (pm) {
+      const unsigned np = static_cast<unsigned>(__popcll(pm));
+      if (ring_n + np > 64u) flush_ring();
+      if (pending) {
+        const unsigned r = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(pm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(pm), 0u));
+        lds_out[wbase + ring_n + r] = cold[256];
+        pending = false;
+      }
+      ring_n += np;
+    }
+  };
+  // Claims the next 64-pixel batch and fills the inbox (all lanes; wave-uniform control). False when
+  // the queue is exhausted.
+  auto claim_batch = [&]() -> bool {
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(queue, BATCH);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= total) return false;
+    // a 64-pixel batch is one tile of one job: the job is wave-uniform here (scalar loads)
+    const unsigned btile = order ? order[base >> 6] : (base >> 6);
+    const int job = (a.n_jobs > 1 && btile >= a.jobs[1].tile_base) + (a.n_jobs > 2 && btile >= a.jobs[2].tile_base);
+    const JobArgs& J = a.jobs[job];
+    const unsigned tile = btile - J.tile_base;
+    const int jj = static_cast<int>((tile % J.tiles_x) * 8u + (lane & 7u));
+    const int ii = static_cast<int>((tile / J.tiles_x) * 8u + (lane >> 3));
+    uint2 px{0u, 0xFFFFFFFFu};
+    float4 d0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (jj < J.reg.w && ii < J.reg.h) {
+      // main(): scr_coord = gl_FragCoord.xy / resolution (shader.frag:515-516)
+      const float sx = (static_cast<float>(J.reg.x0 + jj) + 0.5f) / J.resolution[0];
+      const float sy = (static_cast<float>(region_row(J.reg, ii)) + 0.5f) / J.resolution[1];
+      // ray_drct(), shader.frag:501-505
+      const float mx = (sx - 0.5f) * J.mtr_sizes[0];
+      const float my = (0.5f - sy) * J.mtr_sizes[1];
+      V4 dd = mad(ld4(J.right_drct), mx, mad(ld4(J.top_drct), my, ld4(J.vec_to_mtr)));
+      dd = divs(dd, length(dd));
+      d0 = make_float4(dd.x, dd.y, dd.z, dd.w);
+      px = uint2{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ useed, static_cast<uint32_t>(pack_pixel(jj, ii, job))};
+    }
+    lds_in_d0[threadIdx.x] = d0;
+    lds_in_px[threadIdx.x] = px;
+    return true;
   };
   while (true) {
     RT4_STAMP(t_ph);
@@ -352,59 +416,38 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
       const unsigned long long idle = __ballot(!active);
       if (static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN) {
         RT4_LS(8);
-        if (pending) {
-          flush_pixel();
-          pending = false;
-        }
+        retire();
         const unsigned rank =
             __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(idle >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(idle), 0u));
         const unsigned nidle = static_cast<unsigned>(__popcll(idle));
         unsigned got = 0;
         while (got < nidle) {
-          if (b_next == b_end) {
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(queue, BATCH);
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (base >= total) {
+          if (in_next == 64u) {
+            if (!claim_batch()) {
               exhausted = true;
               break;
             }
-            b_next = base;
-            b_end = min(base + BATCH, total);
+            in_next = 0;
           }
-          const unsigned n = min(nidle - got, b_end - b_next);
-          // a 64-pixel batch is one tile of one job: the job is wave-uniform here (scalar loads)
-          const unsigned btile = order ? order[b_next >> 6] : (b_next >> 6);  // wave-uniform
-          const int job = (a.n_jobs > 1 && btile >= a.jobs[1].tile_base) + (a.n_jobs > 2 && btile >= a.jobs[2].tile_base);
-          const JobArgs& J = a.jobs[job];
+          const unsigned n = min(nidle - got, 64u - in_next);
           if (!active && rank >= got && rank < got + n) {
-            const unsigned idx = b_next + (rank - got);
-            const unsigned tile = btile - J.tile_base;
-            const unsigned l = idx & 63u;
-            const int jj = static_cast<int>((tile % J.tiles_x) * 8u + (l & 7u));
-            const int ii = static_cast<int>((tile / J.tiles_x) * 8u + (l >> 3));
-            if (jj < J.reg.w && ii < J.reg.h) {
-              // main(): scr_coord = gl_FragCoord.xy / resolution (shader.frag:515-516)
-              const float sx = (static_cast<float>(J.reg.x0 + jj) + 0.5f) / J.resolution[0];
-              const float sy = (static_cast<float>(region_row(J.reg, ii)) + 0.5f) / J.resolution[1];
-              rng = RngState{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ useed, useed};
-              // ray_drct(), shader.frag:501-505
-              const float mx = (sx - 0.5f) * J.mtr_sizes[0];
-              const float my = (0.5f - sy) * J.mtr_sizes[1];
-              V4 dd = mad(ld4(J.right_drct), mx, mad(ld4(J.top_drct), my, ld4(J.vec_to_mtr)));
-              dd = divs(dd, length(dd));
-              ray = Ray{focus, dd};
+            const unsigned e = wbase + in_next + (rank - got);
+            const uint2 px = lds_in_px[e];
+            if (px.y != 0xFFFFFFFFu) {
+              const float4 d0 = lds_in_d0[e];
+              rng = RngState{px.x, useed};
+              ray = Ray{focus, V4{d0.x, d0.y, d0.z, d0.w}};
               acc = V3{0.0f, 0.0f, 0.0f};
               T = V3{1.0f, 1.0f, 1.0f};
-              cold[0] = make_float4(dd.x, dd.y, dd.z, dd.w);
-              cold[256] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(pack_pixel(jj, ii, job)));
+              cold[0] = d0;
+              cold[256] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(px.y));
               s = 0;
               b = 0;
               active = NS > 0;
               pending = !active;
             }
           }
-          b_next += n;
+          in_next += n;
           got += n;
         }
       }
@@ -484,7 +527,8 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
       }
     }
   }
-  if (pending) flush_pixel();
+  retire();  // the pixels finished after the queue ran dry, then whatever the ring holds
+  if (ring_n) flush_ring();
 #ifdef RT4_LANESTATS
   if (counter && lane == 0)
     for (int q = 0; q < 20; q++) atomicAdd(counter + 16 + q, ls[q]);
@@ -609,6 +653,9 @@ __global__ void rt4_find_kernel(const rt4_scene_desc* __restrict__ S, const Scen
                                 const float* __restrict__ rays, float* __restrict__ out,
                                 float* __restrict__ out_color, int64_t n) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+#ifdef RT4_LANESTATS
+  rt4_ls_counter = nullptr;  // diagnostic build: only the trace kernel counts
+#endif
   if (t >= n) return;
   const float* r = rays + 8 * t;
   const Ray ray{ld4(r), ld4(r + 4)};
@@ -640,6 +687,9 @@ __global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, cons
                                       const KernelArgs a, unsigned* __restrict__ order, unsigned* __restrict__ ends) {
   const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned n = a.total >> 6;
+#ifdef RT4_LANESTATS
+  rt4_ls_counter = nullptr;  // diagnostic build: only the trace kernel counts
+#endif
   if (t >= n) return;
   const int job = (a.n_jobs > 1 && t >= a.jobs[1].tile_base) + (a.n_jobs > 2 && t >= a.jobs[2].tile_base);
   const JobArgs& J = a.jobs[job];
