@@ -109,6 +109,9 @@ struct Finder {
   static __device__ __forceinline__ Hit resolve(const PrimEntry* P, const Ray& ray, const Cand& c) {
     return rt4::resolve<K>(P, ray, c);
   }
+  static __device__ __forceinline__ float refl(const rt4_scene_desc* __restrict__, const PrimEntry* P, const Cand& c) {
+    return P[c.id].refl;
+  }
   static __device__ __forceinline__ void material(const rt4_scene_desc* __restrict__, const PrimEntry* P, const Hit& h,
                                                   float& glow, float& refl, V3& color) {
     const PrimEntry& e = P[h.mat];
@@ -125,6 +128,9 @@ struct Finder<GENERIC> {
     return find_intersection_generic(S, ray);
   }
   static __device__ __forceinline__ Hit resolve(const PrimEntry*, const Ray&, const Hit& h) { return h; }
+  static __device__ __forceinline__ float refl(const rt4_scene_desc* __restrict__ S, const PrimEntry*, const Hit& h) {
+    return reinterpret_cast<const rt4_material*>(reinterpret_cast<const char*>(S) + h.mat)->refl_prob;
+  }
   static __device__ __forceinline__ void material(const rt4_scene_desc* __restrict__ S, const PrimEntry*, const Hit& h,
                                                   float& glow, float& refl, V3& color) {
     const rt4_material* m = reinterpret_cast<const rt4_material*>(reinterpret_cast<const char*>(S) + h.mat);
@@ -176,10 +182,10 @@ __device__ __forceinline__ float bits_to_rand(uint32_t m) { return __uint_as_flo
 __device__ __forceinline__ float rand_(RngState& r) { return bits_to_rand(rand_bits(r)); }
 
 #if RT4_LUT_PREFETCH
-// Index of the sampler-table entry the next diffuse bounce will read: rand() call #2 after now
-// (#1 is rand_outcome, shader.frag:488; #2 is rand_drct's w, :154). Pure function of the counter.
-__device__ __forceinline__ uint32_t next_diffuse_w_index(const RngState& r) {
-  return hash_u32(r.base ^ (r.iter + 2u * 0x79A010A9u)) & 0x007FFFFFu;
+// Index of the sampler-table entry a diffuse bounce reads once rand_outcome's draw is consumed: the
+// next rand() call (rand_drct's w, shader.frag:154). Pure function of the counter.
+__device__ __forceinline__ uint32_t next_w_index(const RngState& r) {
+  return hash_u32(r.base ^ (r.iter + 0x79A010A9u)) & 0x007FFFFFu;
 }
 #endif
 
@@ -478,11 +484,14 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         end = true;
       } else {
         RT4_LS(4);
+        // rand_outcome's draw first (shader.frag:488, :121; the same draw, taken earlier): only a
+        // diffuse outcome reads the sampler table, so mirrors and reflect outcomes issue no gather
+        const bool diffuse = rand_(rng) > Finder<K>::refl(S, P, c);
 #if RT4_LUT_PREFETCH == 2
 #ifdef RT4_ABL_NOLUT  // ablation only (wrong images): the index arithmetic without the table gather
-        if (LUT) w_pre = WEntry{static_cast<float>(next_diffuse_w_index(rng)) * 2.3841858e-7f - 1.0f};
+        if (LUT && diffuse) w_pre = WEntry{static_cast<float>(next_w_index(rng)) * 2.3841858e-7f - 1.0f};
 #else
-        if (LUT) w_pre = wlut[next_diffuse_w_index(rng)];  // in flight during resolve + shading
+        if (LUT && diffuse) w_pre = wlut[next_w_index(rng)];  // in flight during resolve + shading
 #endif
 #endif
         RT4_STAMP(t_ph);
@@ -495,7 +504,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
         acc = V3{fmaf_(c.x * glow, T.x, acc.x), fmaf_(c.y * glow, T.y, acc.y), fmaf_(c.z * glow, T.z, acc.z)};  // :481
         T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
         ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                  // :485
-        if (!(rand_(rng) > refl)) {  // :488 rand_outcome -> reflect
+        if (!diffuse) {  // :488 rand_outcome -> reflect
           RT4_LS(5);
           const float dn = dot(h.norm, ray.drct);
           ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
