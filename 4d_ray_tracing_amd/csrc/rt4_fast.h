@@ -413,22 +413,21 @@ __device__ __forceinline__ PrimBases prim_bases(const SceneAux* __restrict__ X) 
   }
 }
 
+// find_cand in three parts, so that a kernel can pool the exact sphere tests of several waves between
+// them (rt4_trace.hip, POOL): find_pre = the spaces and the sphere cull (pending-sphere bit mask),
+// sphere_exact = one pending sphere's exact test, find_rest = the groups after the spheres.
 template <uint32_t SH>
-__device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                          const PrimEntry* P, const Ray& ray) {
+__device__ __forceinline__ Cand find_pre(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                         const Ray& ray, uint32_t& pend) {
   constexpr uint32_t K = SH & 0xFFu;
-  constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2), NCY = sh_count(SH, 3);
-  const PrimBases B = prim_bases<SH>(X);
+  constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2);
   Cand inter = no_cand();
+  pend = 0;
   if (K & K_SPACES) for_count<NSP>(S->n_spaces, [&](int i) { inter = closest(space_cand(S, i, ray), inter); });
   if (K & K_SPHERES) {
-#if RT4_SPHERE_CULL
     // Pass 1 (every sphere, ~20 VALU): the exact early-out (outside and pointing away) plus a
-    // conservative "clearly missed" test; only the remaining spheres are marked pending.
-    // Pass 2: each lane evaluates ITS pending spheres in index order, so a wave pays for
-    // max-over-lanes(pending) exact evaluations instead of n_spheres (rt4_aux.h SphereCull for the
-    // error bound that makes the cull exact).
-    uint32_t pend = 0;
+    // conservative "clearly missed" test; only the remaining spheres are marked pending
+    // (rt4_aux.h SphereCull for the error bound that makes the cull exact).
     for_count<NSH>(S->n_spheres, [&](int i) {
       const f8v k = *reinterpret_cast<const f8v*>(&X->sphere_cull[i]);  // one 32-B scalar load
       const V4 po = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
@@ -438,33 +437,24 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
       const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5]));
       pend |= skip ? 0u : (1u << i);
     });
-    while (pend) {
-#ifdef RT4_LANESTATS  // diagnostic: pending-loop trips and their active lanes, per block in LDS
-      {
-        const unsigned long long ex = __builtin_amdgcn_read_exec();
-        // the pointer is set by the trace kernel only: null in the tile-order and find kernels
-        if (rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
-          atomicAdd(rt4_ls_counter + 40, 1ull);
-          atomicAdd(rt4_ls_counter + 41, static_cast<unsigned long long>(__popcll(ex)));
-        }
-      }
-#endif
-      const int i = __builtin_ctz(pend);
-      pend &= pend - 1u;
-      const uint32_t id = B.sphere + static_cast<uint32_t>(i);
-      const PrimEntry& e = P[id];
-      const DivC dc{e.r, e.y, e.fast, 0};
-      inter = closest(sphere_cand(ld4(e.p), e.r, dc, ray, true, id), inter);
-    }
-#else
-    for_count<NSH>(S->n_spheres, [&](int i) {
-      const rt4_sphere& sp = S->spheres[i];
-      inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true,
-                                  B.sphere + static_cast<uint32_t>(i)),
-                      inter);
-    });
-#endif
   }
+  return inter;
+}
+
+template <uint32_t SH>
+__device__ __forceinline__ Cand sphere_exact(const SceneAux* __restrict__ X, const PrimEntry* P, const Ray& ray, int i) {
+  const uint32_t id = prim_bases<SH>(X).sphere + static_cast<uint32_t>(i);
+  const PrimEntry& e = P[id];
+  const DivC dc{e.r, e.y, e.fast, 0};
+  return sphere_cand(ld4(e.p), e.r, dc, ray, true, id);
+}
+
+template <uint32_t SH>
+__device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                          const PrimEntry* P, const Ray& ray, Cand inter) {
+  constexpr uint32_t K = SH & 0xFFu;
+  constexpr uint32_t NCY = sh_count(SH, 3);
+  const PrimBases B = prim_bases<SH>(X);
   if (K & K_CYLINDERS)
     for_count<NCY>(S->n_cylinders, [&](int i) {
       const rt4_cylinder& c = S->cylinders[i];
@@ -479,6 +469,48 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
   if (K & K_TIGER)
     if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
   return inter;
+}
+
+template <uint32_t SH>
+__device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
+                                          const PrimEntry* P, const Ray& ray) {
+  constexpr uint32_t K = SH & 0xFFu;
+#if RT4_SPHERE_CULL
+  uint32_t pend;
+  Cand inter = find_pre<SH>(S, X, ray, pend);
+  if (K & K_SPHERES) {
+    // Pass 2: each lane evaluates ITS pending spheres in index order, so a wave pays for
+    // max-over-lanes(pending) exact evaluations instead of n_spheres.
+    while (pend) {
+#ifdef RT4_LANESTATS  // diagnostic: pending-loop trips and their active lanes, per block in LDS
+      {
+        const unsigned long long ex = __builtin_amdgcn_read_exec();
+        // the pointer is set by the trace kernel only: null in the tile-order and find kernels
+        if (rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+          atomicAdd(rt4_ls_counter + 40, 1ull);
+          atomicAdd(rt4_ls_counter + 41, static_cast<unsigned long long>(__popcll(ex)));
+        }
+      }
+#endif
+      const int i = __builtin_ctz(pend);
+      pend &= pend - 1u;
+      inter = closest(sphere_exact<SH>(X, P, ray, i), inter);
+    }
+  }
+  return find_rest<SH>(S, X, P, ray, inter);
+#else
+  constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2);
+  const PrimBases B = prim_bases<SH>(X);
+  Cand inter = no_cand();
+  if (K & K_SPACES) for_count<NSP>(S->n_spaces, [&](int i) { inter = closest(space_cand(S, i, ray), inter); });
+  if (K & K_SPHERES)
+    for_count<NSH>(S->n_spheres, [&](int i) {
+      const rt4_sphere& sp = S->spheres[i];
+      inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true, B.sphere + static_cast<uint32_t>(i)),
+                      inter);
+    });
+  return find_rest<SH>(S, X, P, ray, inter);
+#endif
 }
 
 // Normal + material of the winning candidate (per-lane data: vector loads from the scene).

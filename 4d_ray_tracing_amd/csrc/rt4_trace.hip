@@ -57,6 +57,12 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_SKY_PRETEST
 #define RT4_SKY_PRETEST 1
 #endif
+#ifndef RT4_POOL_SPHERES
+// Cross-wave pooling of the exact sphere tests (rt4_trace_kernel POOL). Bit-exact, but measured
+// slower: sphere -13 %, room -7 %, all_primitives -21 % (profiles/r02_ab.txt): the four waves must
+// iterate in step, and two barriers per iteration cost more than the denser tests save. Off.
+#define RT4_POOL_SPHERES 0
+#endif
 #ifndef RT4_WAVES_PER_SIMD
 #define RT4_WAVES_PER_SIMD 1
 #endif
@@ -322,6 +328,23 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   }
   const PrimEntry* P = reinterpret_cast<const PrimEntry*>(lds_prims + CELLS4);
 
+  // Cross-wave pooling of the exact sphere tests: in the specialised kernels with
+  // spheres, the four waves of a workgroup iterate in step; each iteration every wave publishes the
+  // rays of its lanes with pending spheres (find_pre's cull) and the (lane, sphere) pairs, and after a
+  // barrier the workgroup's 256 lanes evaluate the pooled pairs densely (one pair per lane) instead
+  // of each wave running the ~190-instruction test on the ~14 of its 64 lanes that need it. Results
+  // are combined by each ray's own lane in sphere index order (closest(), shader.frag:440-441), so
+  // the bits do not change. Up to PCAP lanes per wave are pooled; the rest test their spheres locally.
+  constexpr bool POOL = RT4_POOL_SPHERES && K != GENERIC && (K & K_SPHERES) && sh_count(K, 2) != 0;
+  constexpr int NSH = POOL ? static_cast<int>(sh_count(K, 2)) - 1 : 1;
+  constexpr int PCAP = 32, QCAP = POOL ? PCAP * NSH : 1;
+  __shared__ float4 lds_pray[POOL ? 4 * PCAP * 2 : 1];  // pooled rays: {point, drct} per slot
+  __shared__ uint16_t lds_pair[POOL ? 4 * QCAP : 1];   // slot | sphere << 6
+  __shared__ float2 lds_pres[POOL ? 4 * QCAP : 1];     // {dist, hit | flip << 1}
+  __shared__ uint4 lds_pn4;                            // pairs of each wave | busy << 31, one word per wave
+  uint32_t* const lds_pn = reinterpret_cast<uint32_t*>(&lds_pn4);
+  const unsigned wave = threadIdx.x >> 6;
+
   bool exhausted = false;
   bool active = false, pending = false;
   RngState rng{0u, 0u};
@@ -463,16 +486,90 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     ls[0] += 1;
     ls[1] += __popcll(__ballot(active));
 #endif
-    if (!__any(active)) {
-      if (exhausted) break;
-      continue;
+    typename Finder<K>::R c{};
+    if constexpr (POOL) {
+      // find part 1 + publish; barrier; pooled exact tests; barrier; combine (find part 2 below)
+      RT4_STAMP(t_ph);
+      uint32_t pend = 0;
+      Cand pre = no_cand();
+      if (active) pre = find_pre<K>(S, X, ray, pend);
+      const unsigned long long pm = __ballot(pend != 0u);
+      const unsigned slot = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(pm >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(pm), 0u));
+      const bool pooled = pend != 0u && slot < static_cast<unsigned>(PCAP);
+      if (pooled) {
+        lds_pray[(wave * PCAP + slot) * 2] = make_float4(ray.point.x, ray.point.y, ray.point.z, ray.point.w);
+        lds_pray[(wave * PCAP + slot) * 2 + 1] = make_float4(ray.drct.x, ray.drct.y, ray.drct.z, ray.drct.w);
+      }
+      unsigned nq = 0;  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < NSH; i++) {
+        const unsigned long long qm = __ballot(pooled && ((pend >> i) & 1u));
+        if (pooled && ((pend >> i) & 1u)) {
+          const unsigned q = nq + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(qm >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(qm), 0u));
+          lds_pair[wave * QCAP + q] = static_cast<uint16_t>(slot | (static_cast<unsigned>(i) << 6));
+        }
+        nq += static_cast<unsigned>(__popcll(qm));
+      }
+      const bool busy = __any(active) || !exhausted;
+      if (lane == 0) lds_pn[wave] = nq | (busy ? 0x80000000u : 0u);
+      __syncthreads();
+      const uint4 pn = lds_pn4;
+      if (((pn.x | pn.y | pn.z | pn.w) & 0x80000000u) == 0u) break;  // every wave of the block is done
+      const unsigned c1 = pn.x & 0xFFFFu, c2 = c1 + (pn.y & 0xFFFFu), c3 = c2 + (pn.z & 0xFFFFu);
+      const unsigned ntot = c3 + (pn.w & 0xFFFFu);
+      for (unsigned p = threadIdx.x; p < ntot; p += 256u) {
+        const unsigned w = (p >= c1) + (p >= c2) + (p >= c3);
+        const unsigned j = p - (w == 0u ? 0u : (w == 1u ? c1 : (w == 2u ? c2 : c3)));
+        const unsigned e = lds_pair[w * QCAP + j];
+        const unsigned sl = e & 63u;
+        const float4 rp = lds_pray[(w * PCAP + sl) * 2], rd = lds_pray[(w * PCAP + sl) * 2 + 1];
+        const Cand q = sphere_exact<K>(X, P, Ray{V4{rp.x, rp.y, rp.z, rp.w}, V4{rd.x, rd.y, rd.z, rd.w}},
+                                       static_cast<int>(e >> 6));
+        lds_pres[w * QCAP + j] = make_float2(q.dist, __uint_as_float((q.hit ? 1u : 0u) | (q.flip ? 2u : 0u)));
+      }
+      __syncthreads();
+      if (active) {
+        Cand inter = pre;
+        unsigned nb = 0;  // the pair index of this lane's sphere i: recomputed from the same ballots
+#pragma unroll
+        for (int i = 0; i < NSH; i++) {
+          const bool mine = (pend >> i) & 1u;
+          const unsigned long long qm = __ballot(pooled && mine);
+          if (mine) {
+            Cand q;
+            if (pooled) {
+              const unsigned at = nb + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(qm >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(qm), 0u));
+              const float2 r = lds_pres[wave * QCAP + at];
+              const uint32_t f = __float_as_uint(r.y);
+              q = Cand{(f & 1u) != 0u, (f & 2u) != 0u, r.x, r.x, prim_bases<K>(X).sphere + static_cast<uint32_t>(i)};
+              if (!q.hit) q = no_cand();
+            } else {
+              q = sphere_exact<K>(X, P, ray, i);
+            }
+            inter = closest(q, inter);
+          }
+          nb += static_cast<unsigned>(__popcll(qm));
+        }
+        c = find_rest<K>(S, X, P, ray, inter);
+      }
+      RT4_ACC(1, t_ph);
+    } else {
+      if (!__any(active)) {
+        if (exhausted) break;
+        continue;
+      }
+      if (active) {
+        RT4_STAMP(t_ph);
+        c = Finder<K>::find(S, X, P, ray);  // :475
+        RT4_ACC(1, t_ph);
+      }
     }
     if (active) {
       RT4_LS(1);
-      RT4_STAMP(t_ph);
       WEntry w_pre{};  // sampler-table entry for this iteration's diffuse bounce (LUT path)
-      const typename Finder<K>::R c = Finder<K>::find(S, X, P, ray);  // :475
-      RT4_ACC(1, t_ph);
       ++n_inter;
       bool end;
       if (!c.hit) {  // :477-479
