@@ -71,6 +71,19 @@ __device__ __forceinline__ float sqrt_(float x) {
 }
 __device__ __forceinline__ float length(V4 v) { return sqrt_(dot(v, v)); }
 
+// Division by a per-ray divisor (IEEE, correctly rounded: 11 VALU on gfx950). RT4_ABL_FASTDIV is an
+// ablation build only (NOT exact): reciprocal + one residual step and no check, to bound what an
+// exactness-checked fast quotient could gain at these sites (profiles/r02_ab.txt).
+__device__ __forceinline__ float rdiv(float x, float b) {
+#ifdef RT4_ABL_FASTDIV
+  const float y = __builtin_amdgcn_rcpf(b);
+  const float q = x * y;
+  return fmaf_(fmaf_(-q, b, x), y, q);
+#else
+  return x / b;
+#endif
+}
+
 // ---- transcendentals ------------------------------------------------------------------------
 __device__ __forceinline__ float asin_core(float s, float z) {
   float p = fmaf_(fmaf_(fmaf_(fmaf_(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,

@@ -72,7 +72,7 @@ __device__ __forceinline__ Cand sphere_cand(V4 center, float r, const DivC& dc, 
   if (!(len_po < SMALL_F)) {
     const float dot_pord = dot(vec_po, ray.drct);
     if (len_po >= r && dot_pord < 0.0f) return no_cand();
-    cos_opa = dot_pord / len_po;
+    cos_opa = rdiv(dot_pord, len_po);
     cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
     cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
   }
@@ -103,7 +103,7 @@ __device__ __forceinline__ SphereCore2 sphere_core2(V4 center, float r, const Di
   if (!(c.len_po < SMALL_F)) {
     const float dot_pord = dot(vec_po, ray.drct);
     c.miss = c.len_po >= r && dot_pord < 0.0f;
-    cos_opa = dot_pord / c.len_po;
+    cos_opa = rdiv(dot_pord, c.len_po);
     cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
     cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
   }
@@ -140,7 +140,7 @@ __device__ __forceinline__ Cand space_cand(const rt4_scene_desc* __restrict__ S,
   const float cos_dh = dot(mul(sn, sgn), ray.drct);
   Cand c{true, sgn < 0.0f, 0.0f, 0.0f, static_cast<uint32_t>(i)};
   if (cos_dh < SMALL_F) return no_cand();
-  c.dist = __builtin_fabsf(dot_vn) / cos_dh;
+  c.dist = rdiv(__builtin_fabsf(dot_vn), cos_dh);
   return c;
 }
 
@@ -236,7 +236,7 @@ __device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uin
   const float cos_dn = dot(ray.drct, vec_n);
   if (h < 0.0f || cos_dn < 0.0f) return no_cand();
   if (far && cos_dn * cos_dn >= 1e-12f * l2) return no_cand();  // finite hit point, outside the ball
-  const float dist = h / cos_dn;
+  const float dist = rdiv(h, cos_dn);
   const V4 vec_cp = sub(mad(ray.drct, dist, ray.point), cpt);
   if (__builtin_fabsf(dot(vec_cp, ld4(c.x))) > c.r || __builtin_fabsf(dot(vec_cp, ld4(c.y))) > c.r ||
       __builtin_fabsf(dot(vec_cp, ld4(c.z))) > c.r)
@@ -255,7 +255,7 @@ __device__ __forceinline__ bool cell_hit(const float4* cell, const Ray& ray, flo
   const V4 vec_n = neg(V4{n4.x, n4.y, n4.z, n4.w});
   const float h = dot(sub(cpt, ray.point), vec_n);
   const float cos_dn = dot(ray.drct, vec_n);
-  dist = h / cos_dn;
+  dist = rdiv(h, cos_dn);
   const V4 vec_cp = sub(mad(ray.drct, dist, ray.point), cpt);
   return !(__builtin_fabsf(dot(vec_cp, V4{x4.x, x4.y, x4.z, x4.w})) > r ||
            __builtin_fabsf(dot(vec_cp, V4{y4.x, y4.y, y4.z, y4.w})) > r ||

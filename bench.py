@@ -209,13 +209,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the multi-rank path on a one-GPU box (tests/test_gpu_bench.py): every rank renders on
+    # GPU 0 and the gather / reductions run over gloo on host copies. Never used for a reported number.
+    rehearse = os.environ.get("RT4_BENCH_REHEARSE") == "1"
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if rehearse else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    comm_dev = torch.device("cpu") if rehearse else dev
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     rt4 = importlib.import_module("4d_ray_tracing_amd")
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
 
@@ -227,7 +235,7 @@ def main():
     # setup: context (+ sampler table build) and scene upload (+ divisor / threshold verification)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tracer = rt4.Tracer(device=local_rank, flags=flags)
+    tracer = rt4.Tracer(device=gpu, flags=flags)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     tracer.set_scene(scene)
@@ -279,18 +287,24 @@ def main():
     def render():
         tracer.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, counter.data_ptr(), sptr)
 
+    def gather_once():
+        if rehearse:
+            shard.gather_frame(frame.cpu(), plan, rank)
+        else:
+            shard.gather_frame(frame, plan, rank)  # the frame assembled (un-permuted) on rank 0
+
     def gather():
         g0 = torch.cuda.Event(enable_timing=True)
         g1 = torch.cuda.Event(enable_timing=True)
         g0.record(stream)
-        shard.gather_frame(frame, plan, rank)  # the frame assembled (un-permuted) on rank 0
+        gather_once()
         g1.record(stream)
         gathers.append((g0, g1))
 
     for _ in range(args.warmup):
         render()
         if world > 1 and args.gather == "every":
-            shard.gather_frame(frame, plan, rank)
+            gather_once()
     torch.cuda.synchronize()
     counter.zero_()
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -316,9 +330,9 @@ def main():
 
     n_local = int(counter.item())
     if world > 1:
-        st = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=dev)
+        st = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
-        n_sum = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        n_sum = torch.tensor([n_local], dtype=torch.int64, device=comm_dev)
         dist.all_reduce(n_sum, op=dist.ReduceOp.SUM)
         elapsed, kernel_ms, gather_ms = (float(x) for x in st.tolist())
         n_total = int(n_sum.item())
@@ -340,7 +354,8 @@ def main():
             "height": plan.height, "height_per_gpu": plan.rows_max, "spp": args.spp, "bounces": args.bounces,
             "seed": args.seed, "sampler_lut": not args.no_lut, "frame_format": args.format,
             "progressive": bool(args.progressive), "kernel_version": version,
-            "parallelism": f"pixel-bands x{world}" + (f" + RCCL gather ({args.gather})" if world > 1 else ""),
+            "parallelism": f"pixel-bands x{world}" + (f" + {'gloo rehearsal' if rehearse else 'RCCL'} gather "
+                                                      f"({args.gather})" if world > 1 else ""),
         }
         line = {
             "metric": METRIC,

@@ -44,3 +44,27 @@ def test_bench_strong_config4_one_gpu():
     assert (c["scene"], c["width"], c["height"], c["spp"], c["bounces"]) == ("tiger_two_mirrors", 3840, 2160, 64, 12)
     assert d["efficiency"] == pytest.approx(1.0)
     assert d["intersections_per_step"] <= d["nominal_bound_per_step"]
+
+
+@pytest.mark.parametrize("args", [["--steps", "3", "--warmup", "1"],  # weak, config 2, one gather after the frames
+                                  ["--config", "4", "--steps", "1", "--warmup", "0"]])  # strong, T1 leg, gather per frame
+def test_bench_two_ranks_rehearsal(args):
+    """bench.py --gpus 2 starts two ranks itself (torch.distributed.run) and runs the whole multi-rank
+    path: band plan, per-rank regions, padded gather + un-permute on rank 0, max-over-ranks timing, the
+    strong-scaling T1 leg. On this one-GPU box both ranks render on GPU 0 and the gather runs over gloo
+    (RT4_BENCH_REHEARSE=1); the 8-GPU RCCL run is the driver's."""
+    env = dict(os.environ, RT4_BENCH_REHEARSE="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu-baseline", "--no-ops",
+                        *args], capture_output=True, text=True, timeout=115, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value_per_gpu"] == pytest.approx(d["value"] / 2)
+    assert "gloo rehearsal" in d["config"]["parallelism"] and d["gather_ms"] > 0
+    if "--config" in args:
+        assert d["scaling"] == "strong" and d["t1_ms"] > 0 and 0 < d["efficiency"]
+        assert d["config"]["height"] == 2160 and d["config"]["height_per_gpu"] == 1080
+    else:
+        assert d["scaling"] == "weak" and d["config"]["height"] == 2160
+        assert d["intersections_per_step"] > 2 * 5e7  # both ranks' 1920x1080 shares
