@@ -239,6 +239,7 @@ struct KernelArgs {
   unsigned total;  // 64 x tiles of all jobs
   const unsigned* order;  // queue position -> tile (rt4_tile_order_kernel), or null: row-major
   const unsigned* order_ends;  // the pre-pass's {hit, sky} tile counts (with order)
+  unsigned long long* eval_counter;  // evaluated find_intersection calls (primary-reuse launches), or null
   JobArgs jobs[RT4_MAX_SECTIONS];
 };
 
@@ -248,6 +249,15 @@ __device__ __forceinline__ int region_row(const rt4_region& r, int i) {
 
 // A lane's pixel, packed into one dword of its cold state: region-local j (16 bits) | i (14) | job (2).
 __device__ __forceinline__ int pack_pixel(int j, int i, int job) { return j | (i << 16) | (job << 30); }
+
+// A specialised-kernel candidate in one float4 (the primary-ray cache of RT4_FLAG_PRIMARY_REUSE).
+__device__ __forceinline__ float4 pack_cand(const Cand& c) {
+  return make_float4(c.dist, c.sdist, __uint_as_float((c.hit ? 1u : 0u) | (c.flip ? 2u : 0u) | (c.id << 2)), 0.0f);
+}
+__device__ __forceinline__ Cand unpack_cand(float4 v) {
+  const uint32_t m = __float_as_uint(v.z);
+  return Cand{(m & 1u) != 0u, (m & 2u) != 0u, v.x, v.y, m >> 2};
+}
 
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 
@@ -296,7 +306,7 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
   }
 }
 
-template <uint32_t K, bool LUT>
+template <uint32_t K, bool LUT, bool REUSE>
 __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         unsigned long long* __restrict__ counter,
@@ -353,7 +363,8 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   // Cold per-lane state in LDS, one float4 column per lane (ds_read/write_b128, conflict-free):
   // [0] the pixel's primary direction d0, [256] {light sum, pack_pixel()}. Touched once per sample,
   // so the VGPRs go to occupancy instead (6 -> 7 waves/SIMD on the sphere scene).
-  __shared__ float4 lds_cold[2 * 256];
+  // [512]: the pixel's primary candidate (RT4_FLAG_PRIMARY_REUSE; pack_cand)
+  __shared__ float4 lds_cold[(REUSE ? 3 : 2) * 256];
   float4* const cold = lds_cold + threadIdx.x;
   // Per-wave pixel I/O staged in LDS, 64 entries per wave:
   //   inbox: when the wave claims a 64-pixel batch (one 8x8 tile of one job), all 64 lanes set up the
@@ -370,7 +381,7 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
   unsigned in_next = 64;  // wave-uniform: next inbox entry to hand out (64: empty)
   unsigned ring_n = 0;    // wave-uniform: outbox entries waiting to be written
   int s = 0, b = 0;
-  uint32_t n_inter = 0;
+  uint32_t n_inter = 0, n_eval = 0;  // find_intersection calls of the reference / evaluated here
 
 #ifdef RT4_LANESTATS
   unsigned long long ls[20] = {};
@@ -438,6 +449,54 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     lds_in_d0[threadIdx.x] = d0;
     lds_in_px[threadIdx.x] = px;
     return true;
+  };
+  // One bounce of the lane's path from candidate c (shader.frag:475-492): on a miss the sky term, on a
+  // hit the emitted light, the attenuation, the offset origin and the new direction. True when the
+  // path is finished (a miss, or the bounces ran out: :494).
+  auto shade = [&](const typename Finder<K>::R& c) -> bool {
+    WEntry w_pre{};  // sampler-table entry for this bounce's diffuse direction (LUT path)
+    if (!c.hit) {  // :477-479
+      RT4_LS(3);
+      RT4_STAMP(t_ph);
+      const V3 fl = final_light(S, X, ray.drct);
+      RT4_ACC(2, t_ph);
+      acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
+      return true;
+    }
+    RT4_LS(4);
+    // rand_outcome's draw first (shader.frag:488, :121; the same draw, taken earlier): only a
+    // diffuse outcome reads the sampler table, so mirrors and reflect outcomes issue no gather
+    const bool diffuse = rand_(rng) > Finder<K>::refl(S, P, c);
+#if RT4_LUT_PREFETCH == 2
+#ifdef RT4_ABL_NOLUT  // ablation only (wrong images): the index arithmetic without the table gather
+    if (LUT && diffuse) w_pre = WEntry{static_cast<float>(next_w_index(rng)) * 2.3841858e-7f - 1.0f};
+#else
+    if (LUT && diffuse) w_pre = wlut[next_w_index(rng)];  // in flight during resolve + shading
+#endif
+#endif
+    RT4_STAMP(t_ph);
+    const Hit h = Finder<K>::resolve(P, ray, c);
+    float glow, refl;
+    V3 col;
+    Finder<K>::material(S, P, h, glow, refl, col);
+    RT4_ACC(3, t_ph);
+    acc = V3{fmaf_(col.x * glow, T.x, acc.x), fmaf_(col.y * glow, T.y, acc.y), fmaf_(col.z * glow, T.z, acc.z)};  // :481
+    T = V3{T.x * col.x, T.y * col.y, T.z * col.z};                                                                  // :482
+    ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                          // :485
+    if (!diffuse) {  // :488 rand_outcome -> reflect
+      RT4_LS(5);
+      const float dn = dot(h.norm, ray.drct);
+      ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
+    } else {  // :491 redirect(rand_drct(), norm)
+      RT4_LS(6);
+      RT4_STAMP(t_ph);
+      const V4 v = rand_drct<LUT>(rng, wlut, w_pre);
+      RT4_ACC(4, t_ph);
+      const float dv = dot(v, h.norm);
+      ray.drct = dv >= 0.0f ? v : mad(h.norm, -(2.0f * dv), v);
+    }
+    ++b;
+    return b > R;
   };
   while (true) {
     RT4_STAMP(t_ph);
@@ -569,67 +628,68 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     }
     if (active) {
       RT4_LS(1);
-      WEntry w_pre{};  // sampler-table entry for this iteration's diffuse bounce (LUT path)
       ++n_inter;
-      bool end;
-      if (!c.hit) {  // :477-479
-        RT4_LS(3);
-        RT4_STAMP(t_ph);
-        const V3 fl = final_light(S, X, ray.drct);
-        RT4_ACC(2, t_ph);
-        acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
-        end = true;
-      } else {
-        RT4_LS(4);
-        // rand_outcome's draw first (shader.frag:488, :121; the same draw, taken earlier): only a
-        // diffuse outcome reads the sampler table, so mirrors and reflect outcomes issue no gather
-        const bool diffuse = rand_(rng) > Finder<K>::refl(S, P, c);
-#if RT4_LUT_PREFETCH == 2
-#ifdef RT4_ABL_NOLUT  // ablation only (wrong images): the index arithmetic without the table gather
-        if (LUT && diffuse) w_pre = WEntry{static_cast<float>(next_w_index(rng)) * 2.3841858e-7f - 1.0f};
-#else
-        if (LUT && diffuse) w_pre = wlut[next_w_index(rng)];  // in flight during resolve + shading
-#endif
-#endif
-        RT4_STAMP(t_ph);
-        const Hit h = Finder<K>::resolve(P, ray, c);
-        float glow, refl;
-        V3 col;
-        Finder<K>::material(S, P, h, glow, refl, col);
-        RT4_ACC(3, t_ph);
-        const V3 c = col;
-        acc = V3{fmaf_(c.x * glow, T.x, acc.x), fmaf_(c.y * glow, T.y, acc.y), fmaf_(c.z * glow, T.z, acc.z)};  // :481
-        T = V3{T.x * c.x, T.y * c.y, T.z * c.z};                                                                  // :482
-        ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                  // :485
-        if (!diffuse) {  // :488 rand_outcome -> reflect
-          RT4_LS(5);
-          const float dn = dot(h.norm, ray.drct);
-          ray.drct = mad(h.norm, -(2.0f * dn), ray.drct);
-        } else {  // :491 redirect(rand_drct(), norm)
-          RT4_LS(6);
-          RT4_STAMP(t_ph);
-          const V4 v = rand_drct<LUT>(rng, wlut, w_pre);
-          RT4_ACC(4, t_ph);
-          const float dv = dot(v, h.norm);
-          ray.drct = dv >= 0.0f ? v : mad(h.norm, -(2.0f * dv), v);
-        }
-        ++b;
-        end = b > R;
+      ++n_eval;
+      if constexpr (REUSE) {
+        if (s == 0 && b == 0) cold[512] = pack_cand(c);  // the pixel's primary candidate
       }
-      if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
+      bool end = shade(c);
+      if constexpr (!REUSE) {
+        if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
+          RT4_LS(7);
+          const float4 lp = cold[256];
+          cold[256] = make_float4(lp.x + acc.x, lp.y + acc.y, lp.z + acc.z, lp.w);
+          const float4 c0 = cold[0];
+          ray = Ray{focus, V4{c0.x, c0.y, c0.z, c0.w}};
+          ++s;
+          b = 0;
+          acc = V3{0.0f, 0.0f, 0.0f};
+          T = V3{1.0f, 1.0f, 1.0f};
+          if (s >= NS) {
+            active = false;
+            pending = true;
+          }
+        }
+      }
+      while (REUSE && end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
         RT4_LS(7);
-        const float4 lp = cold[256];
-        cold[256] = make_float4(lp.x + acc.x, lp.y + acc.y, lp.z + acc.z, lp.w);
+        const float4 lp0 = cold[256];
+        float4 lp = make_float4(lp0.x + acc.x, lp0.y + acc.y, lp0.z + acc.z, lp0.w);
         const float4 c0 = cold[0];
         ray = Ray{focus, V4{c0.x, c0.y, c0.z, c0.w}};
         ++s;
         b = 0;
         acc = V3{0.0f, 0.0f, 0.0f};
         T = V3{1.0f, 1.0f, 1.0f};
+        end = false;
         if (s >= NS) {
           active = false;
           pending = true;
+        } else if constexpr (REUSE) {
+          {
+            // RT4_FLAG_PRIMARY_REUSE: every sample of a pixel starts with the same primary ray
+            // (shader.frag:519-521), so its bounce 0 is the cached candidate, shaded in this same
+            // iteration with the sample's own random numbers; no find_intersection is evaluated.
+            const Cand pc = unpack_cand(cold[512]);
+            ++n_inter;
+            if (!pc.hit) {
+              // a primary miss: every remaining sample is that same sky ray, acc = fma(T, sky, acc)
+              // with T = 1, acc = 0 (:477-479), added to the sum sample by sample
+              const V3 fl = final_light(S, X, ray.drct);
+              const V3 m{fmaf_(1.0f, fl.x, 0.0f), fmaf_(1.0f, fl.y, 0.0f), fmaf_(1.0f, fl.z, 0.0f)};
+              lp = make_float4(lp.x + m.x, lp.y + m.y, lp.z + m.z, lp.w);
+              for (++s; s < NS; ++s) {
+                lp = make_float4(lp.x + m.x, lp.y + m.y, lp.z + m.z, lp.w);
+                ++n_inter;
+              }
+              active = false;
+              pending = true;
+            } else {
+              end = shade(pc);  // one bounce; the path goes on next iteration unless bounces ran out
+            }
+          }
         }
+        cold[256] = lp;
       }
     }
   }
@@ -649,6 +709,11 @@ __global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(cons
     unsigned long long v = n_inter;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(counter, v);
+  }
+  if (a.eval_counter) {  // evaluated find calls (fewer than the count above with primary reuse)
+    unsigned long long v = n_eval;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0 && v) atomicAdd(a.eval_counter, v);
   }
 }
 
@@ -821,12 +886,16 @@ typedef void (*OrderFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs
 
 struct Variant {
   uint32_t shape;
-  TraceFn trace[2];  // [lut]
+  TraceFn trace[2][2];  // [lut][primary reuse]
   FindFn find;
   OrderFn order;
 };
 
-#define RT4_VARIANT(K) {K, {rt4_trace_kernel<K, false>, rt4_trace_kernel<K, true>}, rt4_find_kernel<K>, rt4_tile_order_kernel<K>}
+#define RT4_VARIANT(K)                                                                                  \
+  {K,                                                                                                   \
+   {{rt4_trace_kernel<K, false, false>, rt4_trace_kernel<K, false, (K) != GENERIC>},                    \
+    {rt4_trace_kernel<K, true, false>, rt4_trace_kernel<K, true, (K) != GENERIC>}},                     \
+   rt4_find_kernel<K>, rt4_tile_order_kernel<K>}
 // shape | (n_spaces+1) << 8 | (n_spheres+1) << 16 | (n_cylinders+1) << 24 (rt4_fast.h sh_count),
 // from the scene's object counts (the same encoding scene_shape() computes)
 #define SH(K, nsp, nsh, ncy) \
@@ -940,6 +1009,7 @@ struct rt4_context {
   bool launched = false;
   unsigned launch_seq = 0;
   bool queue_dirty = false;  // a launch failed: the next one zeroes its queue word itself
+  unsigned long long* d_eval = nullptr;  // evaluated find calls (RT4_FLAG_PRIMARY_REUSE), rt4_context_evaluated
   int n_cu = 0;
   TraceFn occ_fn = nullptr;  // blocks per CU of the last trace kernel launched (occupancy query cache)
   int occ_per_cu = 0;
@@ -1312,6 +1382,8 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (e == hipSuccess) e = hipMalloc(&c->d_scene, kSceneBytes);
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, (MAX_DIV_SWEEPS + 1) * sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&c->d_queue, QUEUE_SLOTS * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc(&c->d_eval, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->d_eval, 0, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->d_queue, 0, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream's first launch
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
@@ -1345,6 +1417,7 @@ void rt4_context_destroy(rt4_context* ctx) {
   if (ctx->d_order) (void)hipFree(ctx->d_order);
   if (ctx->done) (void)hipEventDestroy(ctx->done);
   if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+  if (ctx->d_eval) (void)hipFree(ctx->d_eval);
   delete ctx;
 }
 
@@ -1428,7 +1501,8 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   a.total = tiles * 64u;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const Variant& v = variant_for(ctx->shape);
-  const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0];
+  const bool reuse = (ctx->flags & RT4_FLAG_PRIMARY_REUSE) && ctx->shape != GENERIC;
+  const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0][reuse ? 1 : 0];
   // grid: what the device holds at once; later blocks would only find the queue empty
   if (ctx->occ_fn != fn) {
     int n = 0;
@@ -1442,6 +1516,7 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   if (blocks < 1) blocks = 1;
   a.order = nullptr;
   a.order_ends = nullptr;
+  if (reuse) a.eval_counter = ctx->d_eval;
   // The tile order buffer is one per context: a launch on another stream than the previous one
   // waits for it (launches of one context run in submission order).
   if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(s, ctx->done, 0));
@@ -1615,6 +1690,17 @@ int rt4_debug_verify_sqrt(rt4_context* ctx, uint64_t* mismatches, char* err, siz
   (void)hipFree(d);
   if (e != hipSuccess) return rt4_set_err(err, errlen, "verify_sqrt failed: %s", hipGetErrorString(e)), RT4_ERR_HIP;
   *mismatches = v;
+  return RT4_OK;
+}
+
+int rt4_context_evaluated(rt4_context* ctx, uint64_t* n, int32_t reset, char* err, size_t errlen) {
+  if (!ctx || !n) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpy(&v, ctx->d_eval, sizeof v, hipMemcpyDeviceToHost));
+  if (reset) HIP_TRY(hipMemset(ctx->d_eval, 0, sizeof v));
+  *n = v;
   return RT4_OK;
 }
 

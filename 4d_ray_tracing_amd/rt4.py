@@ -75,6 +75,7 @@ FINAL_LIGHT_SUN_SKY, FINAL_LIGHT_CONSTANT = 0, 1
 SECTION_YXZ, SECTION_YWZ, SECTION_YXW = 0, 1, 2
 FLAG_SAMPLER_LUT = 0x1
 FLAG_GENERIC_KERNEL = 0x2
+FLAG_PRIMARY_REUSE = 0x4
 FRAME_RGBA32F, FRAME_RGBA16F, FRAME_RGBA8 = 0, 1, 2
 KEY_FORWARD, KEY_BACK, KEY_RIGHT, KEY_LEFT, KEY_UP, KEY_DOWN, KEY_W_POS, KEY_W_NEG = (1 << i for i in range(8))
 MAX_SECTIONS = 3
@@ -191,6 +192,7 @@ def _load():
         "rt4_progressive_uniforms": ([POINTER(Uniforms), c_uint32, POINTER(Uniforms)], c_int),
         "rt4_render_sections_device": ([c_void_p, POINTER(SectionJob), c_int32, c_int32, c_void_p, c_void_p] + E, c_int),
         "rt4_debug_verify_div": ([c_void_p, c_float, c_int32, POINTER(c_uint64)] + E, c_int),
+        "rt4_context_evaluated": ([c_void_p, POINTER(c_uint64), c_int32] + E, c_int),
         "rt4_debug_sky_threshold": ([c_void_p, c_float, c_int32, POINTER(c_float)] + E, c_int),
     }
     tolerant = os.environ.get("RT4_AB_TOLERANT") == "1"  # tools/abtest.sh: older builds lack newer exports
@@ -213,7 +215,7 @@ EXPORTED = (
     "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt "
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
-    "rt4_debug_verify_div rt4_debug_sky_threshold"
+    "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -550,6 +552,13 @@ class Tracer:
         n = c_uint64(0)
         err = _errbuf()
         _check(lib.rt4_debug_verify_sqrt(self._h, ctypes.byref(n), err, len(err)), err)
+        return n.value
+
+    def evaluated(self, reset: bool = True) -> int:
+        """find_intersection calls evaluated by RT4_FLAG_PRIMARY_REUSE launches since the last reset."""
+        n = c_uint64(0)
+        err = _errbuf()
+        _check(lib.rt4_context_evaluated(self._h, ctypes.byref(n), 1 if reset else 0, err, len(err)), err)
         return n.value
 
     def debug_verify_div(self, b: float, full: bool = False) -> int:

@@ -81,6 +81,9 @@ def parse_args(argv=None):
     p.add_argument("--gather", choices=["final", "every"], help="N > 1: RCCL gather once after the frames or per frame")
     p.add_argument("--no-t1", action="store_true", help="strong, N > 1: skip rank 0's whole-frame leg")
     p.add_argument("--no-lut", action="store_true", help="disable the w_by_volume table (inline Newton loop)")
+    p.add_argument("--primary-reuse", action="store_true",
+                   help="RT4_FLAG_PRIMARY_REUSE for the main leg: value becomes reference-equivalent (labelled)")
+    p.add_argument("--no-reuse-leg", action="store_true", help="skip the extra primary-reuse leg (N = 1)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the oracle op count (profiling passes)")
@@ -230,7 +233,7 @@ def main():
     strong = args.mode == "strong"
     plan = shard.make_plan(args.width, args.height, world) if strong else shard.weak_plan(args.width, args.height, world)
     scene = rt4.Scene.named(args.scene)
-    flags = 0 if args.no_lut else rt4.FLAG_SAMPLER_LUT
+    flags = (0 if args.no_lut else rt4.FLAG_SAMPLER_LUT) | (rt4.FLAG_PRIMARY_REUSE if args.primary_reuse else 0)
 
     # setup: context (+ sampler table build) and scene upload (+ divisor / threshold verification)
     torch.cuda.synchronize()
@@ -329,6 +332,39 @@ def main():
     gather_ms = sum(a.elapsed_time(b) for a, b in gathers) / len(gathers) if gathers else 0.0
 
     n_local = int(counter.item())
+    evaluated = tracer.evaluated() if args.primary_reuse else None
+
+    # Extra leg (N = 1): the same frames with RT4_FLAG_PRIMARY_REUSE, reported beside the headline
+    # (a reference-equivalent rate, with the evaluated count next to it).
+    reuse_leg = None
+    if world == 1 and not args.primary_reuse and not args.no_reuse_leg:
+        t_r = rt4.Tracer(device=gpu, flags=flags | rt4.FLAG_PRIMARY_REUSE, scene=scene)
+        frame_no[0] = 0
+        frame.zero_()
+        for _ in range(args.warmup):
+            t_r.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, 0, sptr)
+        torch.cuda.synchronize()
+        t_r.evaluated()  # reset
+        cnt_r = torch.zeros(1, dtype=torch.int64, device=dev)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        tr0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            t_r.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, cnt_r.data_ptr(), sptr)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        el_r = time.perf_counter() - tr0
+        n_r = int(cnt_r.item())
+        reuse_leg = {
+            "label": "reference-equivalent: RT4_FLAG_PRIMARY_REUSE evaluates each pixel's primary ray once and "
+                     "starts its other samples from the cached candidate; same image, same reference count",
+            "value": n_r / el_r, "unit": "ray-bounce intersections/s (reference-equivalent)",
+            "ms_per_step": el_r / args.steps * 1e3, "kernel_ms": ev0.elapsed_time(ev1) / args.steps,
+            "intersections_per_step": n_r / args.steps, "evaluated_per_step": t_r.evaluated() / args.steps,
+        }
+        t_r.close()
     if world > 1:
         st = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
@@ -379,6 +415,12 @@ def main():
             "kernel_ms": kernel_ms,
             "setup_ms": setup,
         }
+        if args.primary_reuse:
+            line["primary_reuse"] = True
+            line["label"] = "reference-equivalent (RT4_FLAG_PRIMARY_REUSE): the primary ray is evaluated once per pixel"
+            line["evaluated_per_step"] = evaluated / args.steps if world == 1 else None
+        if reuse_leg:
+            line["primary_reuse_leg"] = reuse_leg
         if strong:
             line["t1_ms"] = t1_ms if world > 1 else ms_per_step
             line["efficiency"] = (line["t1_ms"] / (world * ms_per_step)) if line["t1_ms"] else None

@@ -295,6 +295,14 @@ typedef struct rt4_context rt4_context;
 /* Always use the generic find_intersection (any group list) instead of the kernel specialised for
  * the scene's shape. Results are identical; used by the tests to cover both code paths. */
 #define RT4_FLAG_GENERIC_KERNEL 0x2u
+/* Primary-ray reuse. Every sample of a pixel starts with the same primary ray (shader.frag:519-521),
+ * so find_intersection of that ray has the same result in all of them: the kernel evaluates it once
+ * per pixel and starts every later sample from the cached candidate (shaded with the sample's own
+ * random numbers, in the iteration that ended the previous sample). Images and the d_counter count
+ * (find_intersection calls of the reference) are unchanged; rt4_context_evaluated reports the calls
+ * actually evaluated. Specialised kernels only (ignored with RT4_FLAG_GENERIC_KERNEL or a generic
+ * scene). SURVEY.md 8(d): a rate measured with it is labelled reference-equivalent. */
+#define RT4_FLAG_PRIMARY_REUSE 0x4u
 
 int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err, size_t errlen);
 /* Uploads a scene (the reference recompiles the shader: src/main.cpp:25-39). Waits for the
@@ -396,6 +404,10 @@ int rt4_debug_find_intersection(rt4_context* ctx, const float* rays, float* out,
 /* Counts the 32-bit patterns x for which the kernel's sqrt (fast path without input scaling) differs
  * from the IEEE square root; 0 expected. Exhaustive over all 2^32 inputs on the device (~10 ms). */
 int rt4_debug_verify_sqrt(rt4_context* ctx, uint64_t* mismatches, char* err, size_t errlen);
+
+/* find_intersection calls the context's launches actually evaluated since the last reset (all of them
+ * unless RT4_FLAG_PRIMARY_REUSE: only its launches count). Waits for the context's last launch. */
+int rt4_context_evaluated(rt4_context* ctx, uint64_t* n, int32_t reset, char* err, size_t errlen);
 
 /* The scene-constant checks of rt4_context_set_scene, alone (synchronous). verify_div: mismatches of
  * the verified-divisor quotient against x / b over the reduced sweep (full = 0: positive numerators,

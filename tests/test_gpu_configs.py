@@ -31,26 +31,33 @@ def bits_equal(a, b):
 
 @pytest.mark.parametrize("name,config", [("sphere", 2), ("hypercube", 3)])
 def test_full_frame_1080p_bitwise(rt4, oracle, name, config):
-    """BASELINE config 2 / 3: every pixel of the 1920x1080 x 16 spp x 8 bounce frame, seed 12345."""
+    """BASELINE config 2 / 3: every pixel of the 1920x1080 x 16 spp x 8 bounce frame, seed 12345, with
+    and without primary-ray reuse (RT4_FLAG_PRIMARY_REUSE: same image, same reference count, fewer
+    evaluated find calls)."""
     import torch
 
     scene = rt4.Scene.named(name)
     u = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
     reg = rt4.region(1920, 1080)
-    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
-    try:
-        fr = torch.zeros((1080, 1920, 4), dtype=torch.float32, device="cuda")
-        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        t.render_device(u, reg, fr.data_ptr(), 1920, cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        g = fr.cpu().numpy()
-    finally:
-        t.close()
     c, nc, _, _ = oracle.render(scene.desc, u, reg, threads=THREADS)
-    assert int(cnt.item()) == nc
-    eq = bits_equal(g, c)
-    assert eq.all(), f"config {config}: {(~eq).sum()} of {eq.size} values differ"
-    assert (g[..., 3] == 1.0).all() and (g[..., :3] >= 0).all() and (g[..., :3] < 1).all()
+    for flags in (rt4.FLAG_SAMPLER_LUT, rt4.FLAG_SAMPLER_LUT | rt4.FLAG_PRIMARY_REUSE):
+        t = rt4.Tracer(device=0, flags=flags, scene=scene)
+        try:
+            fr = torch.zeros((1080, 1920, 4), dtype=torch.float32, device="cuda")
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            t.render_device(u, reg, fr.data_ptr(), 1920, cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            g = fr.cpu().numpy()
+            n_eval = t.evaluated()
+        finally:
+            t.close()
+        assert int(cnt.item()) == nc
+        eq = bits_equal(g, c)
+        assert eq.all(), f"config {config} flags {flags}: {(~eq).sum()} of {eq.size} values differ"
+        assert (g[..., 3] == 1.0).all() and (g[..., :3] >= 0).all() and (g[..., :3] < 1).all()
+        if flags & rt4.FLAG_PRIMARY_REUSE:
+            # 16 primary finds per pixel become one: nc - 15 * W * H evaluated
+            assert n_eval == nc - 15 * 1920 * 1080, (n_eval, nc)
 
 
 def fp16_blend_bound(n):

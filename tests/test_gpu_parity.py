@@ -401,3 +401,59 @@ def test_sky_threshold_sweep_restriction(tracer, rt4):
     for a in sorted(angs):
         r, f = tracer.debug_sky_threshold(a), tracer.debug_sky_threshold(a, full=True)
         assert (np.isnan(r) and np.isnan(f)) or np.float32(r).view(np.uint32) == np.float32(f).view(np.uint32), (a, r, f)
+
+
+# ---------------------------------------------------------------------------- primary-ray reuse
+@pytest.mark.parametrize("name", SCENES)
+@pytest.mark.parametrize("spp,bounces", [(4, 4), (3, 0), (1, 2)])
+def test_primary_reuse_bitwise(rt4, oracle, name, spp, bounces):
+    """RT4_FLAG_PRIMARY_REUSE: the cached primary candidate gives the same image and the same reference
+    count as evaluating it in every sample (bounces = 0: every sample ends at its first bounce; spp = 1:
+    nothing to reuse); evaluated calls = count - (spp - 1) per pixel."""
+    u = rt4.make_uniforms(96, 60, samples=spp, reflections=bounces, seed=4321)
+    reg = rt4.region(96, 60)
+    scene = rt4.Scene.named(name)
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT | rt4.FLAG_PRIMARY_REUSE, scene=scene)
+    try:
+        fg = np.zeros((60, 96, 4), np.float32)
+        ng = t.render_host(u, reg, fg)
+        n_eval = t.evaluated()
+    finally:
+        t.close()
+    fc, nc, _, _ = oracle.render(scene.desc, u, reg)
+    assert ng == nc
+    assert_bits(fg, fc, f"{name} primary reuse")
+    assert n_eval == nc - (spp - 1) * 96 * 60
+
+
+def test_primary_reuse_progressive_and_sections(rt4, oracle):
+    """Reuse across progressive frames (fp16 accumulator) and in a three-section launch."""
+    import torch
+
+    scene = rt4.Scene.named("room")
+    base = rt4.make_uniforms(72, 44, samples=5, reflections=6, seed=77)
+    reg = rt4.region(72, 44)
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT | rt4.FLAG_PRIMARY_REUSE, scene=scene)
+    try:
+        g = np.zeros((44, 72, 4), np.float16)
+        c = np.zeros((44, 72, 4), np.float16)
+        for n in range(1, 4):
+            u = rt4.progressive_uniforms(base, n)
+            ng = t.render_host_ex(u, reg, g, rt4.FRAME_RGBA16F)
+            _, nc = oracle.render_fmt(scene.desc, u, reg, rt4.FRAME_RGBA16F, frame=c)
+            assert ng == nc
+            assert (g.view(np.uint16) == c.view(np.uint16)).all(), n
+        jobs, frames, us = [], [], []
+        for sec, (w, h) in zip((rt4.SECTION_YXZ, rt4.SECTION_YWZ, rt4.SECTION_YXW), [(50, 31), (30, 19), (30, 19)]):
+            u = rt4.make_uniforms(w, h, samples=3, reflections=4, seed=9, section=sec, fi=15.0, te=5.0, psi=20.0)
+            fr = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            frames.append(fr)
+            us.append((u, w, h))
+            jobs.append((u, rt4.region(w, h), fr.data_ptr(), w))
+        t.render_sections_device(jobs)
+        torch.cuda.synchronize()
+        for (u, w, h), fr in zip(us, frames):
+            cc, _, _, _ = oracle.render(scene.desc, u, rt4.region(w, h))
+            assert (fr.cpu().numpy().view(np.uint32) == cc.view(np.uint32)).all()
+    finally:
+        t.close()
