@@ -11,7 +11,7 @@ for c in $CONFIGS; do
     5) steps="--steps 8 --warmup 1" ;;
     *) steps="--steps 5 --warmup 1" ;;
   esac
-  bash "$ROOT/tools/profile.sh" "${TAG}_config$c" --config "$c" $steps --no-cpu-baseline --no-ops || exit 1
+  bash "$ROOT/tools/profile.sh" "${TAG}_config$c" --config "$c" $steps --no-cpu-baseline --no-ops --no-reuse-leg || exit 1
   python3 "$ROOT/tools/pmc_summary.py" "$ROOT/gpurun_out/prof_${TAG}_config$c" > /dev/null || exit 1
   echo "config $c profiled"
 done
