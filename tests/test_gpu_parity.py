@@ -457,3 +457,41 @@ def test_primary_reuse_progressive_and_sections(rt4, oracle):
             assert (fr.cpu().numpy().view(np.uint32) == cc.view(np.uint32)).all()
     finally:
         t.close()
+
+
+def test_find_intersection_hypercube_face_planes(rt4, oracle):
+    """The axis-aligned cell test (rt4_fast.h axis2) against the exact one where they could differ:
+    rays starting exactly on a cell's face plane (h = +-0, whose sign the full dot may flip), rays
+    parallel to a face (cos_dn = 0), zero direction components, and origins on the cell edges."""
+    scene = rt4.Scene.named("hypercube")
+    d = scene.desc
+    rng = np.random.default_rng(17)
+    planes = []
+    for k in range(8):
+        cu = d.hypercubes[0].cubes[k]
+        planes.append((k & 3, cu.point[k & 3], cu.r, list(cu.point)))
+    rays = []
+    for q in range(40000):
+        a, c, r, cpt = planes[q % 8]
+        p = rng.uniform(-3.0, 3.0, 4).astype(np.float32)
+        p[a] = np.float32(c) if q % 3 else -np.float32(c)
+        if q % 5 == 0:  # on an edge of the cell: a second coordinate at +-r from the cell point
+            b = (a + 1 + q % 3) % 4
+            p[b] = np.float32(cpt[b] + (r if q % 2 else -r))
+        dv = rng.normal(size=4).astype(np.float32)
+        if q % 4 == 0:
+            dv[a] = 0.0  # parallel to the face
+        if q % 7 == 0:
+            dv[(a + 2) % 4] = -0.0
+        dv /= np.float32(np.linalg.norm(dv))
+        rays.append(np.concatenate([p, dv]))
+    rays = np.array(rays, np.float32)
+    c, cc = oracle.find_intersection(d, rays)
+    t = rt4.Tracer(device=0, scene=scene)
+    try:
+        g, gc = t.debug_find_intersection(rays)
+    finally:
+        t.close()
+    assert_bits(g, c, "hypercube face-plane find_intersection")
+    assert_bits(gc, cc, "hypercube face-plane colour")
+    assert c[:, 0].sum() > 1000
