@@ -306,8 +306,16 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
   }
 }
 
+// Waves per SIMD the register allocator must leave room for: the tiger kernels with other groups
+// (all_primitives, ~107 VGPRs -> 4 waves) run faster at 5 with a small spill (+3.7 % on config 5,
+// profiles/r02_ab.txt); everything else keeps the allocator's choice.
+constexpr int min_waves_of(uint32_t K) {
+  return (K != GENERIC && (K & K_TIGER) && (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE))) ? 5
+                                                                                                   : RT4_WAVES_PER_SIMD;
+}
+
 template <uint32_t K, bool LUT, bool REUSE>
-__global__ __launch_bounds__(256, RT4_WAVES_PER_SIMD) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
+__global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         unsigned long long* __restrict__ counter,
                                                         const WEntry* __restrict__ wlut, unsigned* __restrict__ queue,
