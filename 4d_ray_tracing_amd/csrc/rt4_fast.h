@@ -92,28 +92,40 @@ struct SphereCore2 {
   bool miss;
   float len_po, angle_opa, angle_oap;
 };
-__device__ __forceinline__ SphereCore2 sphere_core2(V4 center, float r, const DivC& dc, const Ray& ray) {
-  SphereCore2 c;
-  V4 vec_po = sub(center, ray.point);
-  c.len_po = length(vec_po);
+// The cores of the two radii of one tiger axes pair (inner and outer cylinder: same centre, same
+// projected ray): vec_po, len_po, cos_opa, acos(cos_opa) and its sine do not depend on r, so they are
+// evaluated once; each radius keeps its own early-out, its sin_oap (div_c by r) and its asin. The same
+// ops on the same operands as two separate cores, so the same bits.
+__device__ __forceinline__ void sphere_core_pair(V4 center, float r0, const DivC& dc0, float r1, const DivC& dc1,
+                                                 const Ray& ray, SphereCore2& c0, SphereCore2& c1) {
+  const V4 vec_po = sub(center, ray.point);
+  const float len_po = length(vec_po);
   float cos_opa = 0.0f;
-  c.miss = false;
-  c.angle_opa = 0.0f;
-  c.angle_oap = 0.0f;
-  if (!(c.len_po < SMALL_F)) {
+  bool away = false;
+  if (!(len_po < SMALL_F)) {
     const float dot_pord = dot(vec_po, ray.drct);
-    c.miss = c.len_po >= r && dot_pord < 0.0f;
-    cos_opa = rdiv(dot_pord, c.len_po);
+    away = dot_pord < 0.0f;
+    cos_opa = rdiv(dot_pord, len_po);
     cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
     cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
   }
-  if (c.miss) return c;
-  c.angle_opa = acos_(cos_opa);
-  const float sin_oap = div_c(c.len_po * sin_(c.angle_opa), dc);
-  c.miss = sin_oap >= 1.0f;
-  if (c.miss) return c;
-  c.angle_oap = asin_(sin_oap);
-  return c;
+  c0 = SphereCore2{away && len_po >= r0, len_po, 0.0f, 0.0f};
+  c1 = SphereCore2{away && len_po >= r1, len_po, 0.0f, 0.0f};
+  if (c0.miss && c1.miss) return;
+  const float angle_opa = acos_(cos_opa);
+  const float ls = len_po * sin_(angle_opa);
+  if (!c0.miss) {
+    c0.angle_opa = angle_opa;
+    const float sin_oap = div_c(ls, dc0);
+    c0.miss = sin_oap >= 1.0f;
+    if (!c0.miss) c0.angle_oap = asin_(sin_oap);
+  }
+  if (!c1.miss) {
+    c1.angle_opa = angle_opa;
+    const float sin_oap = div_c(ls, dc1);
+    c1.miss = sin_oap >= 1.0f;
+    if (!c1.miss) c1.angle_oap = asin_(sin_oap);
+  }
 }
 __device__ __forceinline__ void sphere_dist2(const SphereCore2& c, float r, float& d_outer, bool& flip_outer,
                                              float& d_inner) {
@@ -181,10 +193,11 @@ __device__ __forceinline__ Cand tiger_pair(V4 cp, V4 a1, V4 a2, float r_in, floa
                                            const Ray& ray, uint32_t id_base) {
   const CylProj p = cyl_project(cp, a1, a2, ray);
   if (p.miss) return no_cand();
-  Cand res;
+  SphereCore2 c_in, c_out;
+  sphere_core_pair(cp, r_in, dc_in, r_out, dc_out, p.r12, c_in, c_out);
+  Cand res = no_cand();
   {
-    res = no_cand();
-    const SphereCore2 c = sphere_core2(cp, r_in, dc_in, p.r12);
+    const SphereCore2& c = c_in;
     if (!c.miss) {
       float d_o, d_i;
       bool f_o;
@@ -199,7 +212,7 @@ __device__ __forceinline__ Cand tiger_pair(V4 cp, V4 a1, V4 a2, float r_in, floa
     }
   }
   {
-    const SphereCore2 c = sphere_core2(cp, r_out, dc_out, p.r12);
+    const SphereCore2& c = c_out;
     if (!c.miss) {
       float d_o, d_i;
       bool f_o;

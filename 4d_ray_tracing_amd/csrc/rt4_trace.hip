@@ -306,12 +306,15 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
   }
 }
 
-// Waves per SIMD the register allocator must leave room for: the tiger kernels with other groups
-// (all_primitives, ~107 VGPRs -> 4 waves) run faster at 5 with a small spill (+3.7 % on config 5,
-// profiles/r02_ab.txt); everything else keeps the allocator's choice.
+// Waves per SIMD the register allocator must leave room for (measured, profiles/r02_ab.txt): the
+// tiger kernels with other groups (all_primitives, ~107 VGPRs -> 4 waves) run faster at 5 with a small
+// spill (+3.7 % on config 5); the tiger kernel specialised for three or more spaces (the mirror room of
+// config 4) at 6 (+2.3 %); the one-space tiger kernel and everything else keep the allocator's choice
+// (a 6-wave bound costs the one-space tiger 1.2 %).
 constexpr int min_waves_of(uint32_t K) {
-  return (K != GENERIC && (K & K_TIGER) && (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE))) ? 5
-                                                                                                   : RT4_WAVES_PER_SIMD;
+  if (K == GENERIC || !(K & K_TIGER)) return RT4_WAVES_PER_SIMD;
+  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return 5;
+  return ((K >> 8) & 0xFFu) >= 4 ? 6 : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
 
 template <uint32_t K, bool LUT, bool REUSE>
