@@ -1175,7 +1175,8 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
   for (int i = 0; i < s.n_spheres; i++) {  // rt4_aux.h SphereCull
     const float r = s.spheres[i].r;
     std::memcpy(a->sphere_cull[i].center, s.spheres[i].center, sizeof a->sphere_cull[i].center);
-    a->sphere_cull[i].d2_out = sqrt_lt_threshold(std::max(r, 0.0003f));  // SMALL_F, shader.frag:24
+    // SMALL_F, shader.frag:24; a NaN radius never takes the exact early-out (len_po >= NaN is false)
+    a->sphere_cull[i].d2_out = std::isnan(r) ? NAN : sqrt_lt_threshold(std::max(r, 0.0003f));
     const bool ok = r >= 1e-15f && r <= 1e15f;  // r <= 0: sin_oap < 1 always, never cull
     a->sphere_cull[i].r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
   }
@@ -1202,6 +1203,10 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     b->r2m = INFINITY;
     const float* ax[4] = {c1.axis1, c1.axis2, c2.axis1, c2.axis2};
     bool ok = same4(c1.point, c2.point) && std::isfinite(r2);
+    // radii in [1e-15, 1e15]: a zero, negative or NaN radius makes sin_oap < -1 possible (a NaN hit
+    // anywhere, found by tests/test_gpu_random_scenes.py test_special_radii), and for tiny radii the
+    // fp32 rounding of r^2 is no longer within the band's 1 %
+    for (int q = 0; q < 4; q++) ok = ok && rr[q] >= 1e-15f && rr[q] <= 1e15f;
     for (int i = 0; i < 4 && ok; i++)
       for (int j = i; j < 4 && ok; j++) {
         double d = 0;

@@ -134,3 +134,34 @@ def test_nonfinite_and_huge_rays(rt4, oracle, name):
         t.close()
     assert_bits(g, c, f"{name} non-finite rays")
     assert_bits(gc, cc, f"{name} non-finite rays colour")
+
+
+SPECIAL_RADII = [float("nan"), 0.0, -0.5, 1e-20, 2e-4, 1e20, float("inf"), 3e-4]
+
+
+@pytest.mark.parametrize("name", ["sphere", "tiger", "cylinder4d", "all_primitives"])
+@pytest.mark.parametrize("radius", SPECIAL_RADII)
+def test_special_radii(rt4, oracle, name, radius):
+    """Spheres, union and tiger cylinders with NaN, zero, negative, tiny, SMALL-sized, huge and infinite
+    radii: the sphere cull and the bounding-ball skips (rt4_aux.h SphereCull, BoundBall) must
+    report exactly what the exact path reports, NaN-distance hits included."""
+    d = rt4.SceneDesc.from_buffer_copy(rt4.Scene.named(name).to_bytes())
+    if d.n_spheres:
+        d.spheres[0].r = radius
+    for i in range(d.n_unions):
+        d.unions[i].cylinder1.r = radius
+    for i in range(d.n_tigers):
+        t = d.tigers[i]
+        t.inner_cyl1.r = radius  # the inner radius of the first axes pair; the other three stay
+        t.outer_cyl2.r = radius if radius != radius else t.outer_cyl2.r
+    scene = rt4.Scene(d)
+    rays = random_rays(20000, 4242)
+    c, cc = oracle.find_intersection(scene.desc, rays)
+    for flags in (0, rt4.FLAG_GENERIC_KERNEL):
+        t = rt4.Tracer(device=0, scene=scene, flags=flags)
+        try:
+            g, gc = t.debug_find_intersection(rays)
+        finally:
+            t.close()
+        assert_bits(g, c, f"{name} r={radius} find_intersection flags={flags}")
+        assert_bits(gc, cc, f"{name} r={radius} colour flags={flags}")
