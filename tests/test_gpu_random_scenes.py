@@ -165,3 +165,37 @@ def test_special_radii(rt4, oracle, name, radius):
             t.close()
         assert_bits(g, c, f"{name} r={radius} find_intersection flags={flags}")
         assert_bits(gc, cc, f"{name} r={radius} colour flags={flags}")
+
+
+@pytest.mark.parametrize("radius", SPECIAL_RADII)
+def test_special_cube_radii(rt4, oracle, radius):
+    """Hypercube cells with special half-sizes: the bounding-ball skip of the faces (rt4_aux.h
+    hyper_bound) and the pending-cell pass must agree with the exact first-hit-in-order test."""
+    d = rt4.SceneDesc.from_buffer_copy(rt4.Scene.named("hypercube").to_bytes())
+    for k in (0, 3, 6):
+        d.hypercubes[0].cubes[k].r = radius
+    scene = rt4.Scene(d)
+    rays = random_rays(20000, 515)
+    c, cc = oracle.find_intersection(scene.desc, rays)
+    for flags in (0, rt4.FLAG_GENERIC_KERNEL):
+        t = rt4.Tracer(device=0, scene=scene, flags=flags)
+        try:
+            g, gc = t.debug_find_intersection(rays)
+        finally:
+            t.close()
+        assert_bits(g, c, f"hypercube r={radius} flags={flags}")
+        assert_bits(gc, cc, f"hypercube r={radius} colour flags={flags}")
+
+
+@pytest.mark.parametrize("ang", [float("nan"), 0.0, -0.1, 1e-30, 1.0, 1.5, 3.2, 100.0, float("inf")])
+def test_special_sun_sizes(rt4, oracle, ang):
+    """Sun angular sizes outside the usual range (NaN, 0, negative, tiny, above 1 and pi, inf): the
+    verified sky threshold, the sky pre-test and the sun division (rt4_aux.h sky_c_star, sky_pre_k,
+    sun_ang) must keep final_light exact. A 64x40 render, 3 spp, 3 bounces."""
+    d = rt4.SceneDesc.from_buffer_copy(rt4.Scene.named("sphere").to_bytes())
+    d.sun.angular_size = ang
+    u = rt4.make_uniforms(64, 40, samples=3, reflections=3, seed=8)
+    reg = rt4.region(64, 40)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene(d), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
+    assert ng == nc
+    assert_bits(fg, fc, f"sun angular size {ang}")
