@@ -91,7 +91,9 @@ struct alignas(64) HotSky {
   float sun_drct[4];   // sun.drct
   float const_rgb[3];  // final_light_const (RT4_FINAL_LIGHT_CONSTANT)
   int32_t mode;        // final_light_mode
-  float pad[4];
+  float pre_a;        // the pre-test's a <= pre_a shortcut: 0 when sky_c_star > 0, else -inf (off; with
+                       // pre_k = 0 the whole pre-test is then off: a sun wider than pi/2 reaches a <= 0)
+  float pad[3];
 };
 
 struct SceneAux {

@@ -156,7 +156,7 @@ __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, 
   const float a_ds = dot(drct, sd), l2 = dot(drct, drct);
 #if RT4_SKY_PRETEST
   // clearly away from the sun: the exact v_cos below would be <= sky_c_star (rt4_aux.h sky_pre_k)
-  if (l2 >= 0x1p-40f && l2 <= 0x1p40f && (a_ds <= 0.0f || a_ds * a_ds < l2 * h[3])) return sky;
+  if (l2 >= 0x1p-40f && l2 <= 0x1p40f && (a_ds <= h[12] || a_ds * a_ds < l2 * h[3])) return sky;
 #endif
   // angle(), :45-50: (dot / length(drct)) / length(sun.drct); the second length is a scene constant
   const float vcos = div_c(a_ds / sqrt_(l2), X->sun_len);
@@ -1329,6 +1329,9 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
   std::memcpy(hs.sun_drct, s.sun.drct, sizeof hs.sun_drct);
   std::memcpy(hs.const_rgb, s.final_light_const, sizeof hs.const_rgb);
   hs.mode = s.final_light_mode;
+  const bool pre_ok = s.final_light_mode == RT4_FINAL_LIGHT_SUN_SKY && a->sky_c_star > 0.0f;  // finite or +inf
+  hs.pre_a = pre_ok ? 0.0f : -INFINITY;
+  if (!pre_ok) hs.pre_k = 0.0f;
   // flat primitive table (rt4_aux.h)
   int n = 0;
   auto add = [&](int kind, const float* p, const float* a1, const float* a2, float r, const DivC& dc,
