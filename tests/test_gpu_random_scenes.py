@@ -199,3 +199,18 @@ def test_special_sun_sizes(rt4, oracle, ang):
     fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene(d), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
     assert ng == nc
     assert_bits(fg, fc, f"sun angular size {ang}")
+
+
+@pytest.mark.parametrize("drct", [(0.0, 0.0, 0.0, 0.0), (float("nan"), 0.0, 1.0, 0.0), (1e30, 0.0, 1e30, 0.0),
+                                  (1e-30, 0.0, 0.0, 0.0), (0.0, -1.0, 0.0, 0.0), (float("inf"), 1.0, 0.0, 0.0)])
+def test_special_sun_directions(rt4, oracle, drct):
+    """Degenerate sun directions (zero, NaN, huge, tiny, straight down, inf): length(sun.drct) is a
+    verified scene divisor (rt4_aux.h sun_len) and scales the sky pre-test constant."""
+    d = rt4.SceneDesc.from_buffer_copy(rt4.Scene.named("sphere").to_bytes())
+    for i in range(4):
+        d.sun.drct[i] = drct[i]
+    u = rt4.make_uniforms(64, 40, samples=3, reflections=3, seed=9)
+    reg = rt4.region(64, 40)
+    fg, ng, fc, nc = render_both(rt4, oracle, rt4.Scene(d), u, reg, flags=rt4.FLAG_SAMPLER_LUT)
+    assert ng == nc
+    assert_bits(fg, fc, f"sun direction {drct}")
