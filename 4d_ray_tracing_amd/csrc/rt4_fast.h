@@ -87,6 +87,29 @@ __device__ __forceinline__ Cand sphere_cand(V4 center, float r, const DivC& dc, 
   return Cand{true, flip, dist, dist, id};
 }
 
+// sphere_cand from d2 = dot(vec_po, vec_po) and dp = dot(vec_po, ray.drct), already evaluated by the
+// cull pass (find_pre) with the same operands and the same op sequence, so the same bits: the exact
+// test then needs neither the centre nor the two dots again.
+__device__ __forceinline__ Cand sphere_cand_d(float d2, float dp, float r, const DivC& dc, bool outer, uint32_t id) {
+  const float len_po = sqrt_(d2);
+  float cos_opa = 0.0f;
+  if (!(len_po < SMALL_F)) {
+    if (len_po >= r && dp < 0.0f) return no_cand();
+    cos_opa = rdiv(dp, len_po);
+    cos_opa = cos_opa > 1.0f ? 1.0f : cos_opa;
+    cos_opa = cos_opa < -1.0f ? -1.0f : cos_opa;
+  }
+  const float angle_opa = acos_(cos_opa);
+  const float sin_oap = div_c(len_po * sin_(angle_opa), dc);
+  if (sin_oap >= 1.0f) return no_cand();
+  float angle_oap = asin_(sin_oap);
+  const bool flip = outer && len_po > r;
+  if (flip) angle_oap = PI_F - angle_oap;
+  const float angle_aop = PI_F - angle_opa - angle_oap;
+  const float dist = sqrt_(r * r + len_po * len_po - 2.0f * r * len_po * cos_(angle_aop));
+  return Cand{true, flip, dist, dist, id};
+}
+
 // Sphere-core shared by the outer=true/false variants of one cylinder face pair.
 struct SphereCore2 {
   bool miss;
@@ -429,9 +452,27 @@ __device__ __forceinline__ PrimBases prim_bases(const SceneAux* __restrict__ X) 
 // find_cand in three parts, so that a kernel can pool the exact sphere tests of several waves between
 // them (rt4_trace.hip, POOL): find_pre = the spaces and the sphere cull (pending-sphere bit mask),
 // sphere_exact = one pending sphere's exact test, find_rest = the groups after the spheres.
+// Exact-count sphere groups of up to GEO_MAX spheres keep the cull's two dots per sphere for the exact
+// test (sphere_cand_d); RT4_SPHERE_GEO=0 recomputes them from the centre (A/B knob). Measured
+// (profiles/r02_ab.txt): sphere scene (2 spheres) +0.7 %; all_primitives (3 spheres, 4 selects per
+// trip, 6 live VGPRs) -0.3 %, so three or more spheres keep the recomputation.
+#ifndef RT4_SPHERE_GEO
+#define RT4_SPHERE_GEO 1
+#endif
+constexpr int GEO_MAX = 2;
+template <uint32_t SH>
+constexpr int geo_spheres() {
+  return (RT4_SPHERE_GEO && ((SH & 0xFFu) & K_SPHERES) && sh_count(SH, 2) != 0 && sh_count(SH, 2) - 1 <= GEO_MAX)
+             ? static_cast<int>(sh_count(SH, 2)) - 1
+             : 0;
+}
+struct SphereGeo {
+  float d2[GEO_MAX], dp[GEO_MAX];
+};
+
 template <uint32_t SH>
 __device__ __forceinline__ Cand find_pre(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
-                                         const Ray& ray, uint32_t& pend) {
+                                         const Ray& ray, uint32_t& pend, SphereGeo* geo = nullptr) {
   constexpr uint32_t K = SH & 0xFFu;
   constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2);
   Cand inter = no_cand();
@@ -446,12 +487,36 @@ __device__ __forceinline__ Cand find_pre(const rt4_scene_desc* __restrict__ S, c
       const V4 po = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
       const float d2 = dot(po, po);  // exactly the dot whose sqrt is len_po in sphere_cand
       const float dp = dot(po, ray.drct);
+      if constexpr (geo_spheres<SH>() > 0) {
+        if (geo) {
+          geo->d2[i] = d2;
+          geo->dp[i] = dp;
+        }
+      }
       const bool outside = d2 >= k[4];  // len_po >= max(r, SMALL)
       const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5]));
       pend |= skip ? 0u : (1u << i);
     });
   }
   return inter;
+}
+
+// The exact test of pending sphere i from the cull's dots (geo_spheres<SH>() > 0): the per-lane sphere
+// index selects its pair of dots with NSH - 1 selects; the primitive entry supplies r and its divisor.
+template <uint32_t SH>
+__device__ __forceinline__ Cand sphere_exact_geo(const SceneAux* __restrict__ X, const PrimEntry* P,
+                                                 const SphereGeo& g, int i) {
+  constexpr int N = geo_spheres<SH>();
+  float d2 = g.d2[0], dp = g.dp[0];
+#pragma unroll
+  for (int k = 1; k < N; k++) {
+    d2 = i == k ? g.d2[k] : d2;
+    dp = i == k ? g.dp[k] : dp;
+  }
+  const uint32_t id = prim_bases<SH>(X).sphere + static_cast<uint32_t>(i);
+  const PrimEntry& e = P[id];
+  const DivC dc{e.r, e.y, e.fast, 0};
+  return sphere_cand_d(d2, dp, e.r, dc, true, id);
 }
 
 template <uint32_t SH>
@@ -490,7 +555,8 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
   constexpr uint32_t K = SH & 0xFFu;
 #if RT4_SPHERE_CULL
   uint32_t pend;
-  Cand inter = find_pre<SH>(S, X, ray, pend);
+  SphereGeo geo;
+  Cand inter = find_pre<SH>(S, X, ray, pend, &geo);
   if (K & K_SPHERES) {
     // Pass 2: each lane evaluates ITS pending spheres in index order, so a wave pays for
     // max-over-lanes(pending) exact evaluations instead of n_spheres.
@@ -507,7 +573,10 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
 #endif
       const int i = __builtin_ctz(pend);
       pend &= pend - 1u;
-      inter = closest(sphere_exact<SH>(X, P, ray, i), inter);
+      if constexpr (geo_spheres<SH>() > 0)
+        inter = closest(sphere_exact_geo<SH>(X, P, geo, i), inter);
+      else
+        inter = closest(sphere_exact<SH>(X, P, ray, i), inter);
     }
   }
   return find_rest<SH>(S, X, P, ray, inter);
