@@ -67,6 +67,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
+#ifndef RT4_WAVES_EXACT
+#define RT4_WAVES_EXACT 6  // exact-count kernels without a tiger (sphere, room, hypercube, cylinder4d): 6 waves/SIMD
+#endif
 #ifndef RT4_WAVES_PER_SIMD
 #define RT4_WAVES_PER_SIMD 1
 #endif
@@ -245,14 +248,25 @@ struct KernelArgs {
   const unsigned* order_ends;  // the pre-pass's {hit, sky} tile counts (with order)
   unsigned long long* eval_counter;  // evaluated find_intersection calls (primary-reuse launches), or null
   JobArgs jobs[RT4_MAX_SECTIONS];
+  // Frames pipelined in one launch (rt4_render_frames_device): n_frames > 1 runs n_frames frames of job 0
+  // through one queue (queue item = frame x tile), frame f with seed frame_seed[f]; a finished pixel's
+  // tone-mapped colour goes to fcolor[f] and rt4_fold_frames_kernel blends the frames in order
+  // (frame_part[f]) into the frame buffer afterwards. Pixel words then pack j | i << 13 | f << 26.
+  int32_t n_frames;
+  unsigned frame_tiles;  // tiles per frame
+  float4* fcolor;        // n_frames x reg.h x reg.w
+  int32_t frame_seed[RT4_MAX_FRAMES];
+  float frame_part[RT4_MAX_FRAMES];
 };
 
 __device__ __forceinline__ int region_row(const rt4_region& r, int i) {
   return r.band_rows > 0 ? r.y0 + (i / r.band_rows) * r.band_step + (i % r.band_rows) : r.y0 + i;
 }
 
-// A lane's pixel, packed into one dword of its cold state: region-local j (16 bits) | i (14) | job (2).
+// A lane's pixel, packed into one dword of its cold state: region-local j (16 bits) | i (14) | job (2);
+// in a pipelined launch (KernelArgs::n_frames > 1) j (13) | i (13) | frame (6).
 __device__ __forceinline__ int pack_pixel(int j, int i, int job) { return j | (i << 16) | (job << 30); }
+__device__ __forceinline__ int pack_pixel_f(int j, int i, int f) { return j | (i << 13) | (f << 26); }
 
 // A specialised-kernel candidate in one float4 (the primary-ray cache of RT4_FLAG_PRIMARY_REUSE).
 __device__ __forceinline__ float4 pack_cand(const Cand& c) {
@@ -265,48 +279,65 @@ __device__ __forceinline__ Cand unpack_cand(float4 v) {
 
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 
-// light /= samples; light_to_color; mix(old_frame, new, part); alpha 1 (shader.frag:522-527), in the
-// launch's frame format (rt4.h rt4_frame_format; the blend is fp32 in every format)
-__device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& J, int pk, V3 light) {
-  const int j = pk & 0xFFFF, i = (pk >> 16) & 0x3FFF;
+// light /= samples; light_to_color (shader.frag:522-526)
+__device__ __forceinline__ V3 tone_map(const KernelArgs& a, V3 light) {
   const float ns = static_cast<float>(a.samples);
   light = V3{light.x / ns, light.y / ns, light.z / ns};
   const float k = a.k;
-  const V3 c{1.0f - 1.0f / fmaf_(k, light.x, 1.0f), 1.0f - 1.0f / fmaf_(k, light.y, 1.0f),
-             1.0f - 1.0f / fmaf_(k, light.z, 1.0f)};
-  const float part = a.part, keep = 1.0f - a.part;
+  return V3{1.0f - 1.0f / fmaf_(k, light.x, 1.0f), 1.0f - 1.0f / fmaf_(k, light.y, 1.0f),
+            1.0f - 1.0f / fmaf_(k, light.z, 1.0f)};
+}
+
+// mix(old_frame, c, part), alpha 1 (shader.frag:527), per frame format (rt4.h rt4_frame_format; the
+// blend is fp32 in every format, then the stored value is rounded). Shared by write_pixel and the
+// fold of pipelined frames, so both run the same ops.
+__device__ __forceinline__ float4 blend_f32(V3 c, float part, float4 old) {
+  const float keep = 1.0f - part;
+  return make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep), fmaf_(c.z, part, old.z * keep),
+                     1.0f);
+}
+__device__ __forceinline__ h4v blend_f16(V3 c, float part, h4v o) {
+  const float keep = 1.0f - part;
+  // the fp32 blend, THEN the rounding to half: the empty asm keeps the backend from fusing the fma
+  // and the conversion into v_fma_mixlo_f16, which rounds once (differs from the contract in the
+  // last half ulp: seen after 256 progressive frames of BASELINE config 5)
+  float b0 = fmaf_(c.x, part, static_cast<float>(o[0]) * keep);
+  float b1 = fmaf_(c.y, part, static_cast<float>(o[1]) * keep);
+  float b2 = fmaf_(c.z, part, static_cast<float>(o[2]) * keep);
+  asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
+  h4v v;
+  v[0] = static_cast<_Float16>(b0);
+  v[1] = static_cast<_Float16>(b1);
+  v[2] = static_cast<_Float16>(b2);
+  v[3] = static_cast<_Float16>(1.0f);
+  return v;
+}
+__device__ __forceinline__ uint32_t blend_u8(V3 c, float part, uint32_t o) {
+  const float keep = 1.0f - part;
+  const float oc[3] = {static_cast<float>(o & 0xFFu) / 255.0f, static_cast<float>((o >> 8) & 0xFFu) / 255.0f,
+                       static_cast<float>((o >> 16) & 0xFFu) / 255.0f};
+  const float nc[3] = {fmaf_(c.x, part, oc[0] * keep), fmaf_(c.y, part, oc[1] * keep), fmaf_(c.z, part, oc[2] * keep)};
+  uint32_t v = 0xFF000000u;
+  for (int q = 0; q < 3; q++) v |= static_cast<uint32_t>(fminf(fmaxf(nc[q], 0.0f), 1.0f) * 255.0f + 0.5f) << (8 * q);
+  return v;
+}
+
+// The pixel's light sum, tone-mapped and blended into the launch's frame (shader.frag:522-527).
+__device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& J, int pk, V3 light) {
+  const int j = pk & 0xFFFF, i = (pk >> 16) & 0x3FFF;
+  const V3 c = tone_map(a, light);
+  const float part = a.part;
   char* base = static_cast<char*>(J.frame);
   const int64_t at = static_cast<int64_t>(i) * J.row_stride_px + j;
   if (a.format == RT4_FRAME_RGBA16F) {
     h4v* px = reinterpret_cast<h4v*>(base) + at;
-    const h4v o = *px;
-    // the fp32 blend, THEN the rounding to half: the empty asm keeps the backend from fusing the fma
-    // and the conversion into v_fma_mixlo_f16, which rounds once (differs from the contract in the
-    // last half ulp: seen after 256 progressive frames of BASELINE config 5)
-    float b0 = fmaf_(c.x, part, static_cast<float>(o[0]) * keep);
-    float b1 = fmaf_(c.y, part, static_cast<float>(o[1]) * keep);
-    float b2 = fmaf_(c.z, part, static_cast<float>(o[2]) * keep);
-    asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
-    h4v v;
-    v[0] = static_cast<_Float16>(b0);
-    v[1] = static_cast<_Float16>(b1);
-    v[2] = static_cast<_Float16>(b2);
-    v[3] = static_cast<_Float16>(1.0f);
-    *px = v;
+    *px = blend_f16(c, part, *px);
   } else if (a.format == RT4_FRAME_RGBA8) {
     uint32_t* px = reinterpret_cast<uint32_t*>(base) + at;
-    const uint32_t o = *px;
-    const float oc[3] = {static_cast<float>(o & 0xFFu) / 255.0f, static_cast<float>((o >> 8) & 0xFFu) / 255.0f,
-                         static_cast<float>((o >> 16) & 0xFFu) / 255.0f};
-    const float nc[3] = {fmaf_(c.x, part, oc[0] * keep), fmaf_(c.y, part, oc[1] * keep), fmaf_(c.z, part, oc[2] * keep)};
-    uint32_t v = 0xFF000000u;
-    for (int q = 0; q < 3; q++) v |= static_cast<uint32_t>(fminf(fmaxf(nc[q], 0.0f), 1.0f) * 255.0f + 0.5f) << (8 * q);
-    *px = v;
+    *px = blend_u8(c, part, *px);
   } else {
     float4* px = reinterpret_cast<float4*>(base) + at;
-    const float4 old = *px;
-    *px = make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep), fmaf_(c.z, part, old.z * keep),
-                      1.0f);
+    *px = blend_f32(c, part, *px);
   }
 }
 
@@ -316,7 +347,8 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
 // config 4) at 6 (+2.3 %); the one-space tiger kernel and everything else keep the allocator's choice
 // (a 6-wave bound costs the one-space tiger 1.2 %).
 constexpr int min_waves_of(uint32_t K) {
-  if (K == GENERIC || !(K & K_TIGER)) return RT4_WAVES_PER_SIMD;
+  if (K == GENERIC) return RT4_WAVES_PER_SIMD;
+  if (!(K & K_TIGER)) return (K >> 8) != 0 ? RT4_WAVES_EXACT : RT4_WAVES_PER_SIMD;  // exact-count shapes: SH() fields
   if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return 5;
   return ((K >> 8) & 0xFFu) >= 4 ? 6 : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
@@ -408,6 +440,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   __shared__ float4 lds_out[256];
   const unsigned wbase = threadIdx.x & ~63u;
   unsigned in_next = 64;  // wave-uniform: next inbox entry to hand out (64: empty)
+  uint32_t in_seed = useed;  // wave-uniform: the seed of the inbox's frame
   unsigned ring_n = 0;    // wave-uniform: outbox entries waiting to be written
   int s = 0, b = 0;
   uint32_t n_inter = 0, n_eval = 0;  // find_intersection calls of the reference / evaluated here
@@ -420,14 +453,25 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, t_loop0, t_ph;
   RT4_STAMP(t_loop0);
 #endif
+#ifdef RT4_TAILSTATS  // diagnostic build only (tools/tailstats.py): per-wave start / queue-empty / exit times
+  const unsigned long long tail_t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tail_exh = 0;
+#endif
   // Writes the outbox ring (lane q takes entry q); one wave-uniform pass per job, so every job's frame
   // pointer and stride stay scalar.
   auto flush_ring = [&]() {
     if (lane < ring_n) {
       const float4 lp = lds_out[wbase + lane];
       const int pk = __float_as_int(lp.w);
-      for (int jb = 0; jb < a.n_jobs; jb++)
-        if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
+      if (a.n_frames > 1) {
+        // pipelined frames: the light sum of frame f as is; rt4_fold_frames_kernel tone-maps and blends
+        const unsigned j = pk & 0x1FFF, i = (pk >> 13) & 0x1FFF, f = (pk >> 26) & 0x3F;  // < 2^28 pixels (4 GiB)
+        const rt4_region& rg = a.jobs[0].reg;
+        a.fcolor[(f * static_cast<unsigned>(rg.h) + i) * static_cast<unsigned>(rg.w) + j] = lp;
+      } else {
+        for (int jb = 0; jb < a.n_jobs; jb++)
+          if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
+      }
     }
     ring_n = 0;
   };
@@ -454,8 +498,14 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     if (lane == 0) base = atomicAdd(queue, BATCH);
     base = __builtin_amdgcn_readfirstlane(base);
     if (base >= total) return false;
-    // a 64-pixel batch is one tile of one job: the job is wave-uniform here (scalar loads)
-    const unsigned btile = order ? order[base >> 6] : (base >> 6);
+    // a 64-pixel batch is one tile of one job (of one frame): wave-uniform here (scalar loads)
+    unsigned pos = base >> 6, frame = 0;
+    if (a.n_frames > 1) {
+      frame = pos / a.frame_tiles;
+      pos -= frame * a.frame_tiles;
+      in_seed = static_cast<uint32_t>(a.frame_seed[frame]);
+    }
+    const unsigned btile = order ? order[pos] : pos;
     const int job = (a.n_jobs > 1 && btile >= a.jobs[1].tile_base) + (a.n_jobs > 2 && btile >= a.jobs[2].tile_base);
     const JobArgs& J = a.jobs[job];
     const unsigned tile = btile - J.tile_base;
@@ -473,7 +523,8 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       V4 dd = mad(ld4(J.right_drct), mx, mad(ld4(J.top_drct), my, ld4(J.vec_to_mtr)));
       dd = divs(dd, length(dd));
       d0 = make_float4(dd.x, dd.y, dd.z, dd.w);
-      px = uint2{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ useed, static_cast<uint32_t>(pack_pixel(jj, ii, job))};
+      px = uint2{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ in_seed,
+                 static_cast<uint32_t>(a.n_frames > 1 ? pack_pixel_f(jj, ii, static_cast<int>(frame)) : pack_pixel(jj, ii, job))};
     }
     lds_in_d0[threadIdx.x] = d0;
     lds_in_px[threadIdx.x] = px;
@@ -542,6 +593,9 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
           if (in_next == 64u) {
             if (!claim_batch()) {
               exhausted = true;
+#ifdef RT4_TAILSTATS
+              tail_exh = __builtin_amdgcn_s_memrealtime();
+#endif
               break;
             }
             in_next = 0;
@@ -552,7 +606,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
             const uint2 px = lds_in_px[e];
             if (px.y != 0xFFFFFFFFu) {
               const float4 d0 = lds_in_d0[e];
-              rng = RngState{px.x, useed};
+              rng = RngState{px.x, in_seed};
               ray = Ray{focus, V4{d0.x, d0.y, d0.z, d0.w}};
               acc = V3{0.0f, 0.0f, 0.0f};
               T = V3{1.0f, 1.0f, 1.0f};
@@ -734,6 +788,14 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     for (int q = 0; q < 6; q++) atomicAdd(counter + 1 + q, st[q]);
 #endif
 
+#ifdef RT4_TAILSTATS
+  if (counter && lane == 0) {  // counter[64 + 3 w ...]: the caller allocates 64 + 3 x (grid waves) words
+    const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    counter[64 + 3 * gw] = tail_t0;
+    counter[64 + 3 * gw + 1] = tail_exh;
+    counter[64 + 3 * gw + 2] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   if (counter) {  // wave-level sum, one atomic per wave
     unsigned long long v = n_inter;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -908,6 +970,38 @@ __global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, cons
   order[pos] = t;
 }
 
+// The frames of a pipelined launch blended in order into the frame buffer (rt4_render_frames_device):
+// per pixel the same blend as write_pixel, frame after frame, each rounded to the frame format.
+__global__ void rt4_fold_frames_kernel(const KernelArgs a) {
+  const JobArgs& J = a.jobs[0];
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t npx = static_cast<int64_t>(J.reg.w) * J.reg.h;
+  if (p >= npx) return;
+  const int i = static_cast<int>(p / J.reg.w), j = static_cast<int>(p - static_cast<int64_t>(i) * J.reg.w);
+  char* base = static_cast<char*>(J.frame);
+  const int64_t at = static_cast<int64_t>(i) * J.row_stride_px + j;
+  auto color = [&](int f) {  // frame f's light sum, tone-mapped as write_pixel does
+    const float4 l = a.fcolor[f * npx + p];
+    return tone_map(a, V3{l.x, l.y, l.z});
+  };
+  if (a.format == RT4_FRAME_RGBA16F) {
+    h4v* px = reinterpret_cast<h4v*>(base) + at;
+    h4v v = *px;
+    for (int f = 0; f < a.n_frames; f++) v = blend_f16(color(f), a.frame_part[f], v);
+    *px = v;
+  } else if (a.format == RT4_FRAME_RGBA8) {
+    uint32_t* px = reinterpret_cast<uint32_t*>(base) + at;
+    uint32_t v = *px;
+    for (int f = 0; f < a.n_frames; f++) v = blend_u8(color(f), a.frame_part[f], v);
+    *px = v;
+  } else {
+    float4* px = reinterpret_cast<float4*>(base) + at;
+    float4 v = *px;
+    for (int f = 0; f < a.n_frames; f++) v = blend_f32(color(f), a.frame_part[f], v);
+    *px = v;
+  }
+}
+
 // ---------------------------------------------------------------- kernel table
 typedef void (*TraceFn)(const rt4_scene_desc*, const SceneAux*, const KernelArgs, unsigned long long*,
                         const WEntry*, unsigned*, unsigned*);
@@ -1031,6 +1125,8 @@ struct rt4_context {
   WEntry* d_wlut = nullptr;
   unsigned* d_queue = nullptr;  // QUEUE_SLOTS words
   unsigned* d_order = nullptr;  // tile order (rt4_tile_order_kernel) + 2 end counters
+  void* d_fcolor = nullptr;     // frame colours of pipelined launches (rt4_render_frames_device)
+  size_t fcolor_bytes = 0;
   size_t order_cap = 0;         // tiles it holds
   bool order_valid = false;     // d_order holds the order for order_args (same scene)
   KernelArgs order_args{};
@@ -1477,6 +1573,7 @@ void rt4_context_destroy(rt4_context* ctx) {
   if (ctx->d_wlut) (void)hipFree(ctx->d_wlut);
   if (ctx->d_queue) (void)hipFree(ctx->d_queue);
   if (ctx->d_order) (void)hipFree(ctx->d_order);
+  if (ctx->d_fcolor) (void)hipFree(ctx->d_fcolor);
   if (ctx->done) (void)hipEventDestroy(ctx->done);
   if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
   if (ctx->d_eval) (void)hipFree(ctx->d_eval);
@@ -1527,8 +1624,16 @@ bool same_shared_uniforms(const rt4_uniforms& a, const rt4_uniforms& b) {
          std::memcmp(a.focus, b.focus, sizeof a.focus) == 0;
 }
 
+// Frames pipelined in one launch (rt4_render_frames_device): per-frame seed and part of job 0.
+struct FramePlan {
+  int32_t n;
+  int32_t cap;  // frames per launch for this frame size: the scratch is sized for cap, once
+  const int32_t* seeds;
+  const float* parts;
+};
+
 int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, int32_t format,
-                unsigned long long* d_counter, void* stream, char* err, size_t errlen) {
+                unsigned long long* d_counter, void* stream, char* err, size_t errlen, const FramePlan* fp = nullptr) {
   if (!ctx || !jobs) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
   if (!ctx->has_scene) return rt4_set_err(err, errlen, "context has no scene (rt4_context_set_scene)"), RT4_ERR_ARG;
   if (n_jobs < 1 || n_jobs > RT4_MAX_SECTIONS)
@@ -1573,6 +1678,20 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   }
   if (tiles == 0) return RT4_OK;
   a.total = tiles * 64u;
+  a.n_frames = 1;
+  const bool frames = fp && fp->n > 1;
+  if (frames) {
+    if (n_jobs != 1 || fp->n > RT4_MAX_FRAMES || a.jobs[0].reg.w > 8191 || a.jobs[0].reg.h > 8191 ||
+        static_cast<uint64_t>(tiles) * 64u * static_cast<uint64_t>(fp->n) >= (1ull << 31))
+      return rt4_set_err(err, errlen, "pipelined frames: bad frame plan"), RT4_ERR_ARG;
+    a.n_frames = fp->n;
+    a.frame_tiles = tiles;
+    a.total = tiles * 64u * static_cast<unsigned>(fp->n);
+    for (int f = 0; f < fp->n; f++) {
+      a.frame_seed[f] = fp->seeds[f];
+      a.frame_part[f] = fp->parts[f];
+    }
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const Variant& v = variant_for(ctx->shape);
   const bool reuse = (ctx->flags & RT4_FLAG_PRIMARY_REUSE) && ctx->shape != GENERIC;
@@ -1586,7 +1705,8 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   }
   const int per_cu = ctx->occ_per_cu;
   long long blocks = static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1);
-  if (blocks > (static_cast<long long>(tiles) + 3) / 4) blocks = (static_cast<long long>(tiles) + 3) / 4;  // >= one tile per wave
+  const long long items = static_cast<long long>(a.total >> 6);  // tiles of all jobs (and frames)
+  if (blocks > (items + 3) / 4) blocks = (items + 3) / 4;  // >= one tile per wave
   if (blocks < 1) blocks = 1;
   a.order = nullptr;
   a.order_ends = nullptr;
@@ -1594,6 +1714,19 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // The tile order buffer is one per context: a launch on another stream than the previous one
   // waits for it (launches of one context run in submission order).
   if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(s, ctx->done, 0));
+  if (frames) {  // the frame colours of a pipelined launch: one scratch buffer per context, grown once
+    const size_t need = static_cast<size_t>(std::max(fp->n, fp->cap)) * static_cast<size_t>(a.jobs[0].reg.w) *
+                        static_cast<size_t>(a.jobs[0].reg.h) * sizeof(float4);
+    if (ctx->fcolor_bytes < need) {
+      HIP_TRY(hipStreamSynchronize(s));
+      if (ctx->d_fcolor) (void)hipFree(ctx->d_fcolor);
+      ctx->d_fcolor = nullptr;
+      ctx->fcolor_bytes = 0;
+      HIP_TRY(hipMalloc(&ctx->d_fcolor, need));
+      ctx->fcolor_bytes = need;
+    }
+    a.fcolor = static_cast<float4*>(ctx->d_fcolor);
+  }
 #if RT4_ORDER_PREPASS
   if (ctx->order_cap < tiles) {  // a frame larger than any before: grow once (allocates)
     HIP_TRY(hipStreamSynchronize(s));
@@ -1607,13 +1740,16 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   unsigned* ends = ctx->d_order + ctx->order_cap;
   // The order depends only on the scene and the primary rays (camera, regions, resolution): a frame
   // that repeats them (progressive accumulation, a benchmark loop) reuses the previous order.
-  if (!(ctx->order_valid && same_primary_rays(ctx->order_args, a))) {
+  KernelArgs ao = a;  // the order is per frame: one frame's tiles
+  ao.total = tiles * 64u;
+  ao.n_frames = 1;
+  if (!(ctx->order_valid && same_primary_rays(ctx->order_args, ao))) {
     ctx->order_valid = false;
     HIP_TRY(hipMemsetAsync(ends, 0, 2 * sizeof(unsigned), s));
-    hipLaunchKernelGGL(v.order, dim3((tiles + 255u) / 256u), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a,
+    hipLaunchKernelGGL(v.order, dim3((tiles + 255u) / 256u), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), ao,
                        ctx->d_order, ends);
     HIP_TRY(hipGetLastError());
-    ctx->order_args = a;
+    ctx->order_args = ao;
     ctx->order_valid = true;
   }
   a.order = ctx->d_order;
@@ -1628,7 +1764,12 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   (void)hipGetLastError();  // a sticky error of an earlier, unrelated call must not be taken for this launch's
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, d_counter,
                      ctx->d_wlut, q, q_next);
-  const hipError_t le = hipGetLastError();
+  hipError_t le = hipGetLastError();
+  if (le == hipSuccess && frames) {
+    const long long npx = static_cast<long long>(a.jobs[0].reg.w) * a.jobs[0].reg.h;
+    hipLaunchKernelGGL(rt4_fold_frames_kernel, dim3(static_cast<unsigned>((npx + 255) / 256)), dim3(256), 0, s, a);
+    le = hipGetLastError();
+  }
   // Record the event whatever happened: a launch that may have been enqueued still orders the next
   // launch on another stream behind it (they share d_order / the queue words).
   const hipError_t re = hipEventRecord(ctx->done, s);
@@ -1660,6 +1801,90 @@ int rt4_render_device_ex(rt4_context* ctx, const rt4_uniforms* u, const rt4_regi
   job.d_frame = d_frame;
   job.row_stride_px = row_stride_px;
   return launch_jobs(ctx, &job, 1, format, d_counter, stream, err, errlen);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Frames per pipelined launch for a w x h region (1: run frame by frame): RT4_MAX_FRAMES, the 4 GiB
+// frame-colour scratch, and queue words below 2^31.
+int32_t frames_per_launch(int32_t w, int32_t h) {
+  if (w <= 0 || h <= 0 || w > 8191 || h > 8191) return 1;
+  const size_t frame_bytes = static_cast<size_t>(w) * static_cast<size_t>(h) * 16u;
+  const size_t tiles = static_cast<size_t>((w + 7) / 8) * static_cast<size_t>((h + 7) / 8);
+  const size_t n = std::min<size_t>({static_cast<size_t>(RT4_MAX_FRAMES), (size_t(4) << 30) / frame_bytes,
+                                     ((size_t(1) << 31) - 1) / (tiles * 64u)});
+  return n < 2 ? 1 : static_cast<int32_t>(n);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rt4_context_frames_per_launch(const rt4_context* ctx, int32_t w, int32_t h) {
+  if (!ctx) return 1;
+  const bool mirror_room = ctx->has_scene && (ctx->shape & 0xFFu) == (K_SPACES | K_TIGER) && ((ctx->shape >> 8) & 0xFFu) >= 4;
+  return mirror_room ? 1 : frames_per_launch(w, h);
+}
+
+int rt4_context_reserve_frames(rt4_context* ctx, int32_t w, int32_t h, char* err, size_t errlen) {
+  if (!ctx) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  const int32_t cap = frames_per_launch(w, h);
+  if (cap < 2) return RT4_OK;
+  const size_t need = static_cast<size_t>(cap) * static_cast<size_t>(w) * static_cast<size_t>(h) * sizeof(float4);
+  if (ctx->fcolor_bytes >= need) return RT4_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
+  if (ctx->d_fcolor) (void)hipFree(ctx->d_fcolor);
+  ctx->d_fcolor = nullptr;
+  ctx->fcolor_bytes = 0;
+  HIP_TRY(hipMalloc(&ctx->d_fcolor, need));
+  HIP_TRY(hipMemset(ctx->d_fcolor, 0, need));  // first touch here, not in the first pipelined launch
+  ctx->fcolor_bytes = need;
+  return RT4_OK;
+}
+
+int rt4_render_frames_device(rt4_context* ctx, const rt4_uniforms* u, int32_t n_frames, const rt4_region* region,
+                             void* d_frame, int32_t format, int64_t row_stride_px, unsigned long long* d_counter,
+                             void* stream, char* err, size_t errlen) {
+  if (!ctx || !u || !region || !d_frame) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  if (n_frames < 1) return rt4_set_err(err, errlen, "n_frames %d < 1", n_frames), RT4_ERR_ARG;
+  for (int32_t f = 1; f < n_frames; f++) {  // only seed and part may change from frame to frame
+    rt4_uniforms x = u[f];
+    x.seed = u[0].seed;
+    x.part = u[0].part;
+    if (std::memcmp(&x, &u[0], sizeof x) != 0)
+      return rt4_set_err(err, errlen, "frame %d: uniforms other than seed/part differ from frame 0", f), RT4_ERR_ARG;
+  }
+  rt4_section_job job;
+  job.u = u[0];
+  job.region = *region;
+  job.d_frame = d_frame;
+  job.row_stride_px = row_stride_px;
+  // The mirror-room tiger kernel (three or more spaces and a tiger: BASELINE config 4) measured slower
+  // pipelined (4K, 64 spp: 128.7 ms per frame against 110.3 ms frame by frame, same clock;
+  // profiles/r02_ab.txt), so its frames run one launch each.
+  const int32_t chunk = rt4_context_frames_per_launch(ctx, region->w, region->h);
+  int32_t seeds[RT4_MAX_FRAMES];
+  float parts[RT4_MAX_FRAMES];
+  for (int32_t f0 = 0; f0 < n_frames; f0 += chunk) {
+    const int32_t n = std::min(chunk, n_frames - f0);
+    int st;
+    if (n == 1) {
+      job.u = u[f0];
+      st = launch_jobs(ctx, &job, 1, format, d_counter, stream, err, errlen);
+    } else {
+      for (int32_t f = 0; f < n; f++) {
+        seeds[f] = u[f0 + f].seed;
+        parts[f] = u[f0 + f].part;
+      }
+      const FramePlan fp{n, chunk, seeds, parts};
+      st = launch_jobs(ctx, &job, 1, format, d_counter, stream, err, errlen, &fp);
+    }
+    if (st != RT4_OK) return st;
+  }
+  return RT4_OK;
 }
 
 int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,

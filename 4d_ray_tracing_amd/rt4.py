@@ -191,6 +191,10 @@ def _load():
                                 POINTER(c_uint64)] + E, c_int),
         "rt4_progressive_uniforms": ([POINTER(Uniforms), c_uint32, POINTER(Uniforms)], c_int),
         "rt4_render_sections_device": ([c_void_p, POINTER(SectionJob), c_int32, c_int32, c_void_p, c_void_p] + E, c_int),
+        "rt4_render_frames_device": ([c_void_p, POINTER(Uniforms), c_int32, POINTER(Region), c_void_p, c_int32, c_int64,
+                                      c_void_p, c_void_p] + E, c_int),
+        "rt4_context_reserve_frames": ([c_void_p, c_int32, c_int32] + E, c_int),
+        "rt4_context_frames_per_launch": ([c_void_p, c_int32, c_int32], c_int32),
         "rt4_debug_verify_div": ([c_void_p, c_float, c_int32, POINTER(c_uint64)] + E, c_int),
         "rt4_context_evaluated": ([c_void_p, POINTER(c_uint64), c_int32] + E, c_int),
         "rt4_debug_sky_threshold": ([c_void_p, c_float, c_int32, POINTER(c_float)] + E, c_int),
@@ -215,7 +219,7 @@ EXPORTED = (
     "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt "
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
-    "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated"
+    "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -494,6 +498,24 @@ class Tracer:
         err = _errbuf()
         _check(lib.rt4_render_device_ex(self._h, byref(u), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
                                         c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
+
+    def render_frames_device(self, us, reg: Region, frame_ptr: int, fmt: int, row_stride_px: int,
+                             counter_ptr: int = 0, stream: int = 0) -> None:
+        """len(us) consecutive frames into one device frame, pipelined (rt4_render_frames_device): the same
+        result as render_device_ex(us[0]), render_device_ex(us[1]), ... in order."""
+        arr = (Uniforms * len(us))(*us)
+        err = _errbuf()
+        _check(lib.rt4_render_frames_device(self._h, arr, len(us), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
+                                            c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
+
+    def frames_per_launch(self, w: int, h: int) -> int:
+        """Frames per pipelined launch for a w x h region with the current scene (1: frame by frame)."""
+        return int(lib.rt4_context_frames_per_launch(self._h, w, h))
+
+    def reserve_frames(self, w: int, h: int) -> None:
+        """Allocate the frame-colour scratch of pipelined launches of a w x h region up front."""
+        err = _errbuf()
+        _check(lib.rt4_context_reserve_frames(self._h, w, h, err, len(err)), err)
 
     def render_sections_device(self, jobs, fmt: int = FRAME_RGBA32F, counter_ptr: int = 0, stream: int = 0) -> None:
         """One launch over up to three images: jobs = [(uniforms, region, frame_ptr, row_stride_px), ...]."""

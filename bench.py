@@ -3,8 +3,10 @@
 
 Workload (BASELINE.json configs[1], SURVEY.md §8(d) config 2, the default): the sphere+plane+sun
 scene (scenes/Шар, плоскость и светилник.frag), 1920x1080 pixels per GPU, 16 samples, 8 reflections,
-seed 12345, default camera, old_frame = 0, part = 1. One "step" = one frame = one launch of the trace
-kernel over the rank's pixels. The unit is one find_intersection() call (shader.frag:475), counted
+seed 12345, default camera, old_frame = 0, part = 1. One "step" = one frame of the rank's pixels; the K
+timed frames go to the library in one rt4_render_frames_device call (frames pipelined through one pixel
+queue, up to 64 per launch, then blended in order: the same final image as K launches), or one launch
+per frame with --frame-by-frame or a gather after every frame. The unit is one find_intersection() call (shader.frag:475), counted
 on the device by the kernel itself. `value` is the whole job's units / time (all ranks);
 `value_per_gpu` divides by the GPU count.
 
@@ -84,6 +86,9 @@ def parse_args(argv=None):
     p.add_argument("--primary-reuse", action="store_true",
                    help="RT4_FLAG_PRIMARY_REUSE for the main leg: value becomes reference-equivalent (labelled)")
     p.add_argument("--no-reuse-leg", action="store_true", help="skip the extra primary-reuse leg (N = 1)")
+    p.add_argument("--frame-by-frame", action="store_true",
+                   help="one launch per frame (rt4_render_device_ex) instead of the pipelined frames of "
+                        "rt4_render_frames_device (always so with a gather after every frame)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the oracle op count (profiling passes)")
@@ -291,19 +296,33 @@ def main():
     sptr = stream.cuda_stream
     counter = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    # ---- T1 leg (strong, N > 1): rank 0 renders the whole frame alone, same warmup/steps
+    # Frames pipelined in one call (rt4_render_frames_device): the same frames, the same final image, the
+    # per-frame drain of the persistent launch paid once per call. Not with a gather after every frame,
+    # which needs every frame's image in the frame buffer.
+    pipelined = not args.frame_by_frame and not (world > 1 and args.gather == "every")
+
+    # ---- T1 leg (strong, N > 1): rank 0 renders the whole frame alone, same warmup/steps and launches
     t1_ms = None
     if strong and world > 1 and not args.no_t1:
         dist.barrier()
         if rank == 0:
             full = torch.zeros((plan.height, plan.width, 4), dtype=tdt, device=dev)
             reg_full = rt4.region(plan.width, plan.height)
-            for _ in range(args.warmup):
-                tracer.render_device_ex(uniforms(), reg_full, full.data_ptr(), fmt, plan.width, 0, sptr)
+            def full_frames(n):
+                if pipelined:
+                    if n:
+                        tracer.render_frames_device([uniforms() for _ in range(n)], reg_full, full.data_ptr(), fmt,
+                                                    plan.width, 0, sptr)
+                    return
+                for _ in range(n):
+                    tracer.render_device_ex(uniforms(), reg_full, full.data_ptr(), fmt, plan.width, 0, sptr)
+
+            if pipelined:
+                tracer.reserve_frames(reg_full.w, reg_full.h)
+            full_frames(args.warmup)
             torch.cuda.synchronize()
             ta = time.perf_counter()
-            for _ in range(args.steps):
-                tracer.render_device_ex(uniforms(), reg_full, full.data_ptr(), fmt, plan.width, 0, sptr)
+            full_frames(args.steps)
             torch.cuda.synchronize()
             t1_ms = (time.perf_counter() - ta) / args.steps * 1e3
             del full
@@ -316,6 +335,9 @@ def main():
 
     def render():
         tracer.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, counter.data_ptr(), sptr)
+
+    def render_frames(n, cnt_ptr):
+        tracer.render_frames_device([uniforms() for _ in range(n)], reg, frame.data_ptr(), fmt, plan.width, cnt_ptr, sptr)
 
     def gather_once():
         if rehearse:
@@ -331,10 +353,15 @@ def main():
         g1.record(stream)
         gathers.append((g0, g1))
 
-    for _ in range(args.warmup):
-        render()
-        if world > 1 and args.gather == "every":
-            gather_once()
+    if pipelined:
+        tracer.reserve_frames(reg.w, reg.h)  # the scratch of the pipelined frames, outside the timed region
+        if args.warmup:
+            render_frames(args.warmup, counter.data_ptr())
+    else:
+        for _ in range(args.warmup):
+            render()
+            if world > 1 and args.gather == "every":
+                gather_once()
     torch.cuda.synchronize()
     counter.zero_()
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -343,19 +370,27 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        k_start[i].record(stream)
-        render()
-        k_end[i].record(stream)
-        if world > 1 and args.gather == "every":
-            gather()
+    if pipelined:
+        k_start[0].record(stream)
+        render_frames(args.steps, counter.data_ptr())
+        k_end[0].record(stream)
+    else:
+        for i in range(args.steps):
+            k_start[i].record(stream)
+            render()
+            k_end[i].record(stream)
+            if world > 1 and args.gather == "every":
+                gather()
     if world > 1 and args.gather == "final":
         gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / args.steps
+    if pipelined:  # per frame: the pipelined launch(es) and the fold, divided by the frames
+        kernel_ms = k_start[0].elapsed_time(k_end[0]) / args.steps
+    else:
+        kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / args.steps
     gather_ms = sum(a.elapsed_time(b) for a, b in gathers) / len(gathers) if gathers else 0.0
 
     n_local = int(counter.item())
@@ -368,8 +403,18 @@ def main():
         t_r = rt4.Tracer(device=gpu, flags=flags | rt4.FLAG_PRIMARY_REUSE, scene=scene)
         frame_no[0] = 0
         frame.zero_()
-        for _ in range(args.warmup):
-            t_r.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, 0, sptr)
+        def reuse_frames(n, cnt_ptr):
+            if pipelined:
+                if n:
+                    t_r.render_frames_device([uniforms() for _ in range(n)], reg, frame.data_ptr(), fmt, plan.width,
+                                             cnt_ptr, sptr)
+                return
+            for _ in range(n):
+                t_r.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, cnt_ptr, sptr)
+
+        if pipelined:
+            t_r.reserve_frames(reg.w, reg.h)
+        reuse_frames(args.warmup, 0)
         torch.cuda.synchronize()
         t_r.evaluated()  # reset
         cnt_r = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -378,8 +423,7 @@ def main():
         torch.cuda.synchronize()
         tr0 = time.perf_counter()
         ev0.record(stream)
-        for _ in range(args.steps):
-            t_r.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, cnt_r.data_ptr(), sptr)
+        reuse_frames(args.steps, cnt_r.data_ptr())
         ev1.record(stream)
         torch.cuda.synchronize()
         el_r = time.perf_counter() - tr0
@@ -402,6 +446,7 @@ def main():
     else:
         n_total = n_local
 
+    fpl = min(args.steps, tracer.frames_per_launch(reg.w, reg.h)) if pipelined else 1
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = n_total / elapsed
@@ -417,6 +462,8 @@ def main():
             "height": plan.height, "height_per_gpu": plan.rows_max, "spp": args.spp, "bounces": args.bounces,
             "seed": args.seed, "sampler_lut": not args.no_lut, "frame_format": args.format,
             "progressive": bool(args.progressive), "kernel_version": version,
+            "launch": (f"{args.steps} frames per rt4_render_frames_device call, {fpl} per pipelined launch"
+                       if pipelined else "one launch per frame (rt4_render_device_ex)"),
             "parallelism": f"pixel-bands x{world}" + (f" + {'gloo rehearsal' if rehearse else 'RCCL'} gather "
                                                       f"({args.gather})" if world > 1 else ""),
         }
@@ -440,6 +487,7 @@ def main():
             "intersections_per_step": n_total / args.steps,
             "nominal_bound_per_step": plan.width * plan.height * args.spp * (args.bounces + 1),
             "kernel_ms": kernel_ms,
+            "frames_per_launch": fpl,
             "setup_ms": setup,
         }
         if args.primary_reuse:

@@ -383,6 +383,31 @@ typedef struct rt4_section_job {
 int rt4_render_sections_device(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, int32_t format,
                                unsigned long long* d_counter, void* stream, char* err, size_t errlen);
 
+/* n_frames consecutive frames into the same frame buffer, pipelined: the same result, bit for bit, as
+ * n_frames calls of rt4_render_device_ex with u[0], u[1], ... in order (the frame loop of main.cpp:57-111
+ * while the camera rests: progressive accumulation, or a benchmark loop), and d_counter receives the
+ * sum of their counts. u[f] may differ from u[0] only in seed and part (rt4_progressive_uniforms);
+ * RT4_ERR_ARG otherwise. The frames share one pixel queue (item = frame x 8x8 tile), so the drain at the
+ * end of a launch (each lane finishing its last pixel's samples in order) is paid once per up to
+ * RT4_MAX_FRAMES frames instead of once per frame. Each pixel's tone-mapped colour of every frame goes
+ * to a context-owned scratch buffer (16 B per pixel and frame, up to 4 GiB: the frames are split into
+ * launches that fit), then one pass blends the frames in order into d_frame with the same per-frame ops
+ * and roundings as rt4_render_device_ex. The intermediate frames are not stored in d_frame. Regions
+ * wider or taller than 8191 pixels run frame by frame. Asynchronous like rt4_render_device_ex; the first
+ * call with a larger scratch need allocates (synchronises the stream once). */
+#define RT4_MAX_FRAMES 64
+int rt4_render_frames_device(rt4_context* ctx, const rt4_uniforms* u, int32_t n_frames, const rt4_region* region,
+                             void* d_frame, int32_t format, int64_t row_stride_px, unsigned long long* d_counter,
+                             void* stream, char* err, size_t errlen);
+/* Allocates (and first-touches) the frame-colour scratch that pipelined launches of a w x h region use,
+ * so that the first rt4_render_frames_device call of that size neither allocates nor synchronises.
+ * Waits for the context's launches in flight when it has to grow the buffer. */
+int rt4_context_reserve_frames(rt4_context* ctx, int32_t w, int32_t h, char* err, size_t errlen);
+/* Frames per pipelined launch rt4_render_frames_device uses for a w x h region with the context's
+ * current scene (1: frame by frame). The mirror-room tiger kernel (three or more spaces and a tiger)
+ * runs frame by frame: it measured slower pipelined. */
+int32_t rt4_context_frames_per_launch(const rt4_context* ctx, int32_t w, int32_t h);
+
 /* ---- diagnostics (used by the parity tests; not on the render path) ------------------------- */
 enum rt4_eval_fn {
   RT4_EVAL_ACOS = 0, RT4_EVAL_ASIN = 1, RT4_EVAL_SIN = 2, RT4_EVAL_COS = 3,

@@ -95,6 +95,17 @@ def main():
             lines = [l for l in open(lp) if l.startswith("{")]
             if lines:
                 b = json.loads(lines[-1])
+                fpl = b.get("frames_per_launch", 1)
+                if fpl > 1 and out.get("avg_ns"):  # pipelined frames (bench --warmup 0): one dispatch = fpl frames
+                    out["frames_per_dispatch"] = fpl
+                    out["avg_ns"] /= fpl
+                    for k in ("min_ns", "max_ns"):
+                        out[k] /= fpl
+                    for k in list(c):
+                        c[k] /= fpl
+                    for k in ("hbm_read_bytes_corrected", "hbm_write_bytes", "hbm_bytes_per_launch", "fabric_read_requests"):
+                        if k in m:
+                            m[k] /= fpl
                 out["config"] = b["config"]
                 out["bench"] = {k: b[k] for k in ("value", "kernel_ms", "intersections_per_step")}
                 if out.get("avg_ns"):
