@@ -67,6 +67,12 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
+#ifndef RT4_WAVES_MIRROR
+#define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
+#endif
+#ifndef RT4_PIPE_MIRROR
+#define RT4_PIPE_MIRROR 0  // 1: pipeline the mirror-room kernel's frames too (A/B knob)
+#endif
 #ifndef RT4_WAVES_EXACT
 #define RT4_WAVES_EXACT 6  // exact-count kernels without a tiger (sphere, room, hypercube, cylinder4d): 6 waves/SIMD
 #endif
@@ -350,7 +356,7 @@ constexpr int min_waves_of(uint32_t K) {
   if (K == GENERIC) return RT4_WAVES_PER_SIMD;
   if (!(K & K_TIGER)) return (K >> 8) != 0 ? RT4_WAVES_EXACT : RT4_WAVES_PER_SIMD;  // exact-count shapes: SH() fields
   if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return 5;
-  return ((K >> 8) & 0xFFu) >= 4 ? 6 : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
+  return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
 
 template <uint32_t K, bool LUT, bool REUSE>
@@ -1824,7 +1830,8 @@ extern "C" {
 
 int32_t rt4_context_frames_per_launch(const rt4_context* ctx, int32_t w, int32_t h) {
   if (!ctx) return 1;
-  const bool mirror_room = ctx->has_scene && (ctx->shape & 0xFFu) == (K_SPACES | K_TIGER) && ((ctx->shape >> 8) & 0xFFu) >= 4;
+  const bool mirror_room = !RT4_PIPE_MIRROR && ctx->has_scene && (ctx->shape & 0xFFu) == (K_SPACES | K_TIGER) &&
+                           ((ctx->shape >> 8) & 0xFFu) >= 4;
   return mirror_room ? 1 : frames_per_launch(w, h);
 }
 
