@@ -73,6 +73,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_PIPE_MIRROR
 #define RT4_PIPE_MIRROR 0  // 1: pipeline the mirror-room kernel's frames too (A/B knob)
 #endif
+#ifndef RT4_WAVES_SPHERE
+#define RT4_WAVES_SPHERE 7
+#endif
 #ifndef RT4_WAVES_EXACT
 #define RT4_WAVES_EXACT 6  // exact-count kernels without a tiger (sphere, room, hypercube, cylinder4d): 6 waves/SIMD
 #endif
@@ -354,7 +357,13 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
 // (a 6-wave bound costs the one-space tiger 1.2 %).
 constexpr int min_waves_of(uint32_t K) {
   if (K == GENERIC) return RT4_WAVES_PER_SIMD;
-  if (!(K & K_TIGER)) return (K >> 8) != 0 ? RT4_WAVES_EXACT : RT4_WAVES_PER_SIMD;  // exact-count shapes: SH() fields
+  if (!(K & K_TIGER)) {
+    if ((K >> 8) == 0) return RT4_WAVES_PER_SIMD;  // runtime counts
+    // the one-space sphere kernel (BASELINE config 2): 7 waves (72 VGPRs, 16 B/lane spill) measured
+    // +1-2.5 % over 6 with pipelined frames; the hypercube kernel -1.3 % at 7 (profiles/r02_ab.txt)
+    if ((K & 0xFFu) == (K_SPACES | K_SPHERES) && ((K >> 8) & 0xFFu) == 2) return RT4_WAVES_SPHERE;
+    return RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
+  }
   if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return 5;
   return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
