@@ -9,6 +9,7 @@
 //   windowGroup->display()                        -> rt4_write_ppm after the last frame
 // Usage: rt4_render [-p properties.txt] [-s scene(.frag|builtin name)] [-n frames] [-3] [-W width -H height]
 //                   [-f f32|f16|rgba8] [--seed S] [-o prefix] [-d device] [--keys WASD...] [--move-seconds t]
+//                   [--frame-by-frame]  (one section and a resting camera: rt4_render_frames_device unless given)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -57,7 +58,7 @@ uint32_t keys_from(const char* s) {  // controls.cpp:98-113 key names
 int main(int argc, char** argv) {
   std::string props_path = "properties.txt", scene_arg, out = "frame", fmt_name = "f32";
   int frames = 1, device = 0, width = 0, height = 0;
-  bool three = false;
+  bool three = false, frame_by_frame = false;
   uint32_t seed = 12345, keys = 0;
   float move_seconds = 0.0f;
   for (int i = 1; i < argc; i++) {
@@ -77,6 +78,7 @@ int main(int argc, char** argv) {
     else if (a == "-o") out = next();
     else if (a == "-d") device = std::atoi(next());
     else if (a == "--keys") keys = keys_from(next());
+    else if (a == "--frame-by-frame") frame_by_frame = true;
     else if (a == "--move-seconds") move_seconds = static_cast<float>(std::atof(next()));
     else die("unknown argument", a.c_str());
   }
@@ -135,8 +137,26 @@ int main(int argc, char** argv) {
   HIP_CHECK(hipEventCreate(&e0));
   HIP_CHECK(hipEventCreate(&e1));
 
+  // One section and a resting camera (progressive accumulation): the frames go to the library in one
+  // rt4_render_frames_device call (pipelined through one pixel queue; the same final image).
+  const bool pipelined = n_img == 1 && !(keys && move_seconds > 0.0f) && !frame_by_frame;
+  std::vector<rt4_uniforms> us;
+  if (pipelined) {
+    RT4_CHECK(rt4_context_reserve_frames(ctx, cw[0], ch[0], err, sizeof err));
+    for (int n = 1; n <= frames; n++) {
+      rt4_uniforms u;
+      RT4_CHECK(rt4_camera_frame_uniforms(&cam, &base[0], sections[0],
+                                          static_cast<int32_t>(seed ^ (static_cast<uint32_t>(n) * 0x9E3779B9u)), &u));
+      us.push_back(u);
+    }
+  }
   HIP_CHECK(hipEventRecord(e0, nullptr));
-  for (int n = 1; n <= frames; n++) {
+  if (pipelined) {
+    const rt4_region reg{0, 0, cw[0], ch[0], 0, 0};
+    RT4_CHECK(rt4_render_frames_device(ctx, us.data(), frames, &reg, d_frame[0], format, cw[0], d_count, nullptr, err,
+                                       sizeof err));
+  }
+  for (int n = 1; n <= frames && !pipelined; n++) {
     const int32_t s_n = static_cast<int32_t>(seed ^ (static_cast<uint32_t>(n) * 0x9E3779B9u));
     rt4_section_job jobs[3];
     const uint32_t frame_number = cam.frame_number;

@@ -143,3 +143,24 @@ def test_mirror_room_runs_frame_by_frame(rt4):
     (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, rt4.FLAG_SAMPLER_LUT)
     assert np_ == nq
     assert same_bits(p, q)
+
+
+@pytest.mark.parametrize("fmt", ["f16", "rgba8"])
+def test_cpp_host_pipelined_equals_frame_by_frame(rt4, tmp_path, fmt):
+    """lib/rt4_render with one section and a resting camera hands its frames to rt4_render_frames_device;
+    its PPM equals the frame-by-frame loop's byte for byte (same intersection count printed)."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(rt4.LIB_PATH), "rt4_render")
+    props = os.path.join(os.path.dirname(rt4.LIB_PATH), "..", "..", "properties.txt")
+    outs = []
+    for extra in ([], ["--frame-by-frame"]):
+        pre = str(tmp_path / ("fbf" if extra else "pipe"))
+        cmd = [exe, "-p", props, "-s", "hypercube", "-n", "5", "-W", "72", "-H", "40", "-f", fmt,
+               "--seed", "77", "-o", pre] + extra
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        count = [ln for ln in r.stdout.splitlines() if "intersections" in ln][0].split("intersections ")[1].split(",")[0]
+        outs.append((open(pre + "_yxz.ppm", "rb").read(), count))
+    assert outs[0] == outs[1]
