@@ -518,10 +518,11 @@ def main():
                 "algorithmic_bytes_per_launch": reg.w * reg.h * 2 * rt4.frame_format_bytes(fmt),  # old_frame in, new out
                 "note": "fp32 ops (fma=2) per find_intersection+shading counted by the oracle on a row sample of "
                         "the frame; executed = without the w_by_volume Newton ops the sampler table replaces; "
-                        "see DESIGN.md §5",
+                        "per launch = per frame (a pipelined launch holds frames_per_launch frames: its units, "
+                        "bytes and time are divided by them); see DESIGN.md §5",
             }
             if src:
-                line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per launch)"
+                line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per frame)"
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(rt4, scene, base, plan.width, plan.rows_max, args.cpu_seconds, cpus)
         print(json.dumps(line), flush=True)
