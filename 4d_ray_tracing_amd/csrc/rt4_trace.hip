@@ -1743,6 +1743,10 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
     a.fcolor = static_cast<float4*>(ctx->d_fcolor);
   }
 #if RT4_ORDER_PREPASS
+  // Pipelined frames keep row-major order: the longest-first order only shortens the drain at the end
+  // of a launch, which a pipelined launch pays once, and in the main phase row-major measured faster
+  // (config 2 +1.5 %, config 3 +2 %; profiles/r02_ab.txt).
+  if (!frames) {
   if (ctx->order_cap < tiles) {  // a frame larger than any before: grow once (allocates)
     HIP_TRY(hipStreamSynchronize(s));
     if (ctx->d_order) (void)hipFree(ctx->d_order);
@@ -1769,6 +1773,7 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   }
   a.order = ctx->d_order;
   a.order_ends = ends;
+  }
 #endif
   unsigned* q = ctx->d_queue + (ctx->launch_seq % QUEUE_SLOTS);
   unsigned* q_next = ctx->d_queue + (++ctx->launch_seq % QUEUE_SLOTS);  // zeroed by this launch
