@@ -26,6 +26,18 @@ struct V3 { float x, y, z; };
 
 __device__ __forceinline__ float fmaf_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// Native-math mode (-DRT4_NATIVE_MATH, a diagnostic build: DESIGN.md §6): the GLSL built-ins of the
+// shader come from ocml (acosf, asinf, sinf, cosf) and the shader's multiply-add forms are evaluated as
+// written, a*b + c with two roundings, instead of the fixed deterministic definition below. It measures
+// how far the images move with the built-ins' definition, the one thing the unrunnable GL reference
+// leaves open. sfma_ is a multiply-add written in the shader; fmaf_ stays an exact fma
+// where an algorithm needs one (correctly rounded sqrt and quotient, conservative bounds).
+#ifdef RT4_NATIVE_MATH
+__device__ __forceinline__ float sfma_(float a, float b, float c) { return a * b + c; }
+#else
+__device__ __forceinline__ float sfma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+#endif
+
 __device__ __forceinline__ V4 make4(float x, float y, float z, float w) { return V4{x, y, z, w}; }
 __device__ __forceinline__ V4 ld4(const float* p) { return V4{p[0], p[1], p[2], p[3]}; }
 __device__ __forceinline__ V3 ld3(const float* p) { return V3{p[0], p[1], p[2]}; }
@@ -35,10 +47,10 @@ __device__ __forceinline__ V4 mul(V4 a, float s) { return V4{a.x * s, a.y * s, a
 __device__ __forceinline__ V4 divs(V4 a, float s) { return V4{a.x / s, a.y / s, a.z / s, a.w / s}; }
 __device__ __forceinline__ V4 neg(V4 a) { return V4{-a.x, -a.y, -a.z, -a.w}; }
 __device__ __forceinline__ V4 mad(V4 a, float s, V4 c) {  // a*s + c
-  return V4{fmaf_(a.x, s, c.x), fmaf_(a.y, s, c.y), fmaf_(a.z, s, c.z), fmaf_(a.w, s, c.w)};
+  return V4{sfma_(a.x, s, c.x), sfma_(a.y, s, c.y), sfma_(a.z, s, c.z), sfma_(a.w, s, c.w)};
 }
 __device__ __forceinline__ float dot(V4 a, V4 b) {
-  return fmaf_(a.w, b.w, fmaf_(a.z, b.z, fmaf_(a.y, b.y, a.x * b.x)));
+  return sfma_(a.w, b.w, sfma_(a.z, b.z, sfma_(a.y, b.y, a.x * b.x)));
 }
 #ifndef RT4_FAST_SQRT
 #define RT4_FAST_SQRT 1
@@ -91,6 +103,16 @@ __device__ __forceinline__ float asin_core(float s, float z) {
   return fmaf_(p, z * s, s);
 }
 
+#ifdef RT4_NATIVE_MATH
+__device__ __forceinline__ float asin_(float x) { return asinf(x); }
+__device__ __forceinline__ float acos_(float x) { return acosf(x); }
+__device__ __forceinline__ float sin_(float x) { return sinf(x); }
+__device__ __forceinline__ float cos_(float x) { return cosf(x); }
+__device__ __forceinline__ void sincos_(float x, float& sv, float& cv) {
+  sv = sinf(x);
+  cv = cosf(x);
+}
+#else
 // Branch-free form of the oracle's rt4m_asin: both arms compute the same op sequence per lane.
 __device__ __forceinline__ float asin_(float x) {
   float a = __builtin_fabsf(x);
@@ -152,6 +174,7 @@ __device__ __forceinline__ void sincos_(float x, float& sv, float& cv) {
   sv = (q & 2) ? -vs : vs;
   cv = ((q + 1) & 2) ? -vc : vc;
 }
+#endif  // RT4_NATIVE_MATH
 
 // ---- RNG (shader.frag:90-121) -----------------------------------------------------------------
 __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {  // :94-102

@@ -6,6 +6,7 @@
 //   * scene loader for the GLSL subset used by scenes/<name>.frag and executable/shader.frag:412-468
 //   * the reference's five scenes as built-ins
 // Compiled with -ffp-contract=off: every fp32 expression is evaluated exactly as written.
+#include <algorithm>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -449,6 +450,29 @@ int rt4_camera_frame_uniforms(rt4_camera* cam, const rt4_uniforms* base, int sec
   if (rt4_section_basis(&cam->orientation, section, u.top_drct, u.right_drct) != RT4_OK) return RT4_ERR_ARG;
   cam->frame_number++;                                           // frameNumber++ (main.cpp:88)
   *out = u;
+  return RT4_OK;
+}
+
+// ============================================================================ multi-GPU pixel bands
+// Bands of `band` rows dealt round-robin over the ranks (shard.py make_plan is the same
+// arithmetic, tests/test_shard.py compares the two). Band b holds image rows [b band, min((b+1) band, H))
+// and belongs to rank b mod world; the rank's local row i is image row
+// (i / band) band world + rank band + i mod band, the rt4_region band layout with y0 = rank band.
+int rt4_band_plan(int32_t width, int32_t height, int32_t world, int32_t band, int32_t rank, rt4_region* region,
+                  int32_t* rows_max, char* err, size_t errlen) {
+  if (!region || !rows_max) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  if (width < 1 || height < 1 || world < 1 || band < 1)
+    return rt4_set_err(err, errlen, "band plan: width %d, height %d, world %d, band %d must be >= 1", width, height,
+                       world, band),
+           RT4_ERR_ARG;
+  if (rank < 0 || rank >= world) return rt4_set_err(err, errlen, "rank %d not in [0, %d)", rank, world), RT4_ERR_ARG;
+  *rows_max = static_cast<int32_t>(rt4_band_rows_max(height, world, band));
+  if (world == 1) {
+    *region = rt4_region{0, 0, width, height, 0, 0};
+  } else {
+    *region = rt4_region{0, rank * band, width, static_cast<int32_t>(rt4_band_rows(height, world, band, rank)), band,
+                         band * world};
+  }
   return RT4_OK;
 }
 

@@ -7,15 +7,26 @@
 //   seed ^= generateSeed(timer); part = 1/frame    -> seed ^ n*0x9E3779B9 (deterministic), camera uniforms
 //   windowGroup->drawShaderImage()                -> rt4_render_sections_device (one launch, 1 or 3 images)
 //   windowGroup->display()                        -> rt4_write_ppm after the last frame
+//   one GL draw of the whole texture (windows.cpp:45) -> with --gpus N: the frame's pixel bands over N GPUs,
+//                                                    one host thread per device, each rank's frames in one
+//                                                    rt4_render_frames_device call, one RCCL ncclGather of the
+//                                                    padded shards to GPU 0 over xGMI, rt4_bands_unpermute_device
 // Usage: rt4_render [-p properties.txt] [-s scene(.frag|builtin name)] [-n frames] [-3] [-W width -H height]
 //                   [-f f32|f16|rgba8] [--seed S] [-o prefix] [-d device] [--keys WASD...] [--move-seconds t]
 //                   [--frame-by-frame]  (one section and a resting camera: rt4_render_frames_device unless given)
+//                   [--gpus N [--band B]]  (one section, resting camera: bands over devices 0..N-1 + RCCL gather)
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt4.h"
@@ -36,6 +47,143 @@ namespace {
     hipError_t e_ = (call);                                             \
     if (e_ != hipSuccess) die(#call, hipGetErrorString(e_));            \
   } while (0)
+
+// A reusable barrier for the device threads (C++17 has no std::barrier).
+class Barrier {
+ public:
+  explicit Barrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const long gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, count_ = 0;
+  long gen_ = 0;
+};
+
+struct BandRun {  // one GPU's share of a --gpus run
+  std::string error;
+  unsigned long long count = 0;
+  double ms = 0.0;  // this rank's wall time from the start barrier to its gather (and, on rank 0, the un-permute)
+};
+
+// The frames of one section on `gpus` devices: pixel bands dealt round-robin
+// (rt4_band_plan), each rank's frames pipelined in one rt4_render_frames_device call into a padded
+// shard of rows_max rows, one ncclGather of the shards to rank 0 and rt4_bands_unpermute_device there.
+// The image equals a one-GPU render bit for bit (every pixel is independent: shader.frag:104-108).
+// Returns the frame on the host (rank 0's), or exits on an error.
+std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc* scene, const std::vector<rt4_uniforms>& us,
+                                        int32_t w, int32_t h, int32_t format, bool frame_by_frame,
+                                        unsigned long long* count_out, double* ms_out) {
+  const int32_t px = rt4_frame_format_bytes(format);
+  std::vector<ncclComm_t> comms(static_cast<size_t>(gpus));
+  std::vector<int> devs(static_cast<size_t>(gpus));
+  for (int r = 0; r < gpus; r++) devs[static_cast<size_t>(r)] = r;
+  if (ncclCommInitAll(comms.data(), gpus, devs.data()) != ncclSuccess) die("ncclCommInitAll", "failed");
+  std::vector<BandRun> runs(static_cast<size_t>(gpus));
+  std::vector<unsigned char> image(static_cast<size_t>(w) * h * px);
+  Barrier bar(gpus);
+  auto rank_main = [&](int r) {
+    BandRun& run = runs[static_cast<size_t>(r)];
+    char err[1024] = {0};
+    rt4_context* ctx = nullptr;
+    void *shard = nullptr, *gathered = nullptr, *img = nullptr;
+    unsigned long long* d_count = nullptr;
+    hipStream_t stream = nullptr;
+    rt4_region reg;
+    int32_t rows_max = 0;
+    bool ok = hipSetDevice(r) == hipSuccess && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) run.error = "hipSetDevice / hipStreamCreate";
+    if (ok && (rt4_band_plan(w, h, gpus, band, r, &reg, &rows_max, err, sizeof err) != RT4_OK ||
+               rt4_context_create(r, RT4_FLAG_SAMPLER_LUT, &ctx, err, sizeof err) != RT4_OK ||
+               rt4_context_set_scene(ctx, scene, err, sizeof err) != RT4_OK)) {
+      ok = false;
+      run.error = err;
+    }
+    const size_t shard_bytes = static_cast<size_t>(rows_max) * w * px;
+    if (ok) {
+      ok = hipMalloc(&shard, shard_bytes) == hipSuccess && hipMemset(shard, 0, shard_bytes) == hipSuccess &&
+           hipMalloc(&d_count, sizeof *d_count) == hipSuccess && hipMemset(d_count, 0, sizeof *d_count) == hipSuccess;
+      if (ok && r == 0)
+        ok = hipMalloc(&gathered, shard_bytes * gpus) == hipSuccess && hipMalloc(&img, image.size()) == hipSuccess;
+      if (!ok) run.error = "device allocation";
+    }
+    const bool pipelined = !frame_by_frame && us.size() >= 2 && reg.h > 0 &&
+                           rt4_context_frames_per_launch(ctx, reg.w, reg.h) > 1;
+    if (ok && pipelined && rt4_context_reserve_frames(ctx, reg.w, reg.h, err, sizeof err) != RT4_OK) {
+      ok = false;
+      run.error = err;
+    }
+    if (ok) ok = hipDeviceSynchronize() == hipSuccess;
+    bar.wait();  // every rank set up: start together
+    const auto t0 = std::chrono::steady_clock::now();
+    if (ok && reg.h > 0) {
+      int st = RT4_OK;
+      if (pipelined) {
+        st = rt4_render_frames_device(ctx, us.data(), static_cast<int32_t>(us.size()), &reg, shard, format, w, d_count,
+                                      stream, err, sizeof err);
+      } else {
+        for (size_t f = 0; f < us.size() && st == RT4_OK; f++)
+          st = rt4_render_device_ex(ctx, &us[f], &reg, shard, format, w, d_count, stream, err, sizeof err);
+      }
+      if (st != RT4_OK) {
+        ok = false;
+        run.error = err;
+      }
+    }
+    // every rank takes part in the gather, also one with an error (its shard is then zeros), so that no
+    // rank waits forever in the collective; the error is reported after it
+    if (ncclGather(shard, gathered, shard_bytes, ncclUint8, 0, comms[static_cast<size_t>(r)], stream) != ncclSuccess &&
+        ok) {
+      ok = false;
+      run.error = "ncclGather failed";
+    }
+    if (ok && r == 0 &&
+        rt4_bands_unpermute_device(gathered, img, w, h, gpus, band, rows_max, format, stream, err, sizeof err) != RT4_OK) {
+      ok = false;
+      run.error = err;
+    }
+    if (hipStreamSynchronize(stream) != hipSuccess && ok) {
+      ok = false;
+      run.error = "hipStreamSynchronize";
+    }
+    run.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ok && hipMemcpy(&run.count, d_count, sizeof run.count, hipMemcpyDeviceToHost) != hipSuccess) run.error = "count";
+    if (ok && r == 0 && hipMemcpy(image.data(), img, image.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      run.error = "image copy";
+    if (shard) (void)hipFree(shard);
+    if (gathered) (void)hipFree(gathered);
+    if (img) (void)hipFree(img);
+    if (d_count) (void)hipFree(d_count);
+    if (stream) (void)hipStreamDestroy(stream);
+    rt4_context_destroy(ctx);
+  };
+  std::vector<std::thread> threads;
+  for (int r = 0; r < gpus; r++) threads.emplace_back(rank_main, r);
+  for (auto& t : threads) t.join();
+  for (auto& c : comms) (void)ncclCommDestroy(c);
+  unsigned long long count = 0;
+  double ms = 0.0;
+  for (int r = 0; r < gpus; r++) {
+    const BandRun& run = runs[static_cast<size_t>(r)];
+    if (!run.error.empty()) die(("rank " + std::to_string(r)).c_str(), run.error.c_str());
+    count += run.count;
+    ms = std::max(ms, run.ms);  // the job's time: the slowest rank
+  }
+  *count_out = count;
+  *ms_out = ms;
+  return image;
+}
 
 uint32_t keys_from(const char* s) {  // controls.cpp:98-113 key names
   uint32_t k = 0;
@@ -59,6 +207,7 @@ int main(int argc, char** argv) {
   std::string props_path = "properties.txt", scene_arg, out = "frame", fmt_name = "f32";
   int frames = 1, device = 0, width = 0, height = 0;
   bool three = false, frame_by_frame = false;
+  int gpus = 0, band = 8;
   uint32_t seed = 12345, keys = 0;
   float move_seconds = 0.0f;
   for (int i = 1; i < argc; i++) {
@@ -80,6 +229,8 @@ int main(int argc, char** argv) {
     else if (a == "--keys") keys = keys_from(next());
     else if (a == "--frame-by-frame") frame_by_frame = true;
     else if (a == "--move-seconds") move_seconds = static_cast<float>(std::atof(next()));
+    else if (a == "--gpus") gpus = std::atoi(next());
+    else if (a == "--band") band = std::atoi(next());
     else die("unknown argument", a.c_str());
   }
   const int32_t format = fmt_name == "f16" ? RT4_FRAME_RGBA16F : fmt_name == "rgba8" ? RT4_FRAME_RGBA8 : RT4_FRAME_RGBA32F;
@@ -121,6 +272,33 @@ int main(int argc, char** argv) {
   rt4_camera cam;
   RT4_CHECK(rt4_camera_init(props, &cam, err, sizeof err));
 
+  if (gpus > 0) {  // pixel bands over GPUs 0..gpus-1, one RCCL gather (one section, resting camera)
+    if (three || (keys && move_seconds > 0.0f)) die("--gpus", "needs one section and a resting camera");
+    if (frames < 1 || band < 1) die("--gpus", "frames and band must be >= 1");
+    int ndev = 0;
+    HIP_CHECK(hipGetDeviceCount(&ndev));
+    if (gpus > ndev) die("--gpus", ("only " + std::to_string(ndev) + " HIP devices").c_str());
+    std::vector<rt4_uniforms> us;
+    for (int n = 1; n <= frames; n++) {
+      rt4_uniforms u;
+      RT4_CHECK(rt4_camera_frame_uniforms(&cam, &base[0], sections[0],
+                                          static_cast<int32_t>(seed ^ (static_cast<uint32_t>(n) * 0x9E3779B9u)), &u));
+      us.push_back(u);
+    }
+    unsigned long long count = 0;
+    double ms = 0.0;
+    const std::vector<unsigned char> img =
+        render_bands(gpus, band, scene, us, cw[0], ch[0], format, frame_by_frame, &count, &ms);
+    const std::string path = out + "_yxz.ppm";
+    RT4_CHECK(rt4_write_ppm(path.c_str(), img.data(), format, cw[0], ch[0], cw[0], err, sizeof err));
+    std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[0], ch[0]);
+    std::printf("gpus %d, frames %d, images 1, intersections %llu, %.3f ms/frame, %.3e intersections/s\n", gpus,
+                frames, count, ms / frames, static_cast<double>(count) / (ms * 1e-3));
+    rt4_properties_free(props);
+    std::free(scene);
+    return 0;
+  }
+
   rt4_context* ctx = nullptr;
   RT4_CHECK(rt4_context_create(device, RT4_FLAG_SAMPLER_LUT, &ctx, err, sizeof err));
   RT4_CHECK(rt4_context_set_scene(ctx, scene, err, sizeof err));
@@ -142,7 +320,10 @@ int main(int argc, char** argv) {
   const bool pipelined = n_img == 1 && !(keys && move_seconds > 0.0f) && !frame_by_frame;
   std::vector<rt4_uniforms> us;
   if (pipelined) {
-    RT4_CHECK(rt4_context_reserve_frames(ctx, cw[0], ch[0], err, sizeof err));
+    // the frame-colour scratch only when frames are actually pipelined (>= 2 frames, a scene that does
+    // not run frame by frame), and only for the frames of one chunk
+    if (frames >= 2 && rt4_context_frames_per_launch(ctx, cw[0], ch[0]) > 1)
+      RT4_CHECK(rt4_context_reserve_frames(ctx, cw[0], ch[0], err, sizeof err));
     for (int n = 1; n <= frames; n++) {
       rt4_uniforms u;
       RT4_CHECK(rt4_camera_frame_uniforms(&cam, &base[0], sections[0],

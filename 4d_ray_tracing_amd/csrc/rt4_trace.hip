@@ -16,6 +16,14 @@
 //   * optional w_by_volume table (RT4_FLAG_SAMPLER_LUT): the Newton loop of shader.frag:141-150
 //     is a pure function of rand()'s 23 mantissa bits; a 2^23-entry table built by the same
 //     device function replaces the divergent loop by one cached load.
+#ifdef RT4_NATIVE_MATH
+// Native-math diagnostic build (rt4_device_math.h): the exact shortcuts whose proofs assume the
+// deterministic built-ins are compiled out, so the kernel evaluates the shader's expressions plainly.
+#define RT4_SPHERE_CULL 0
+#define RT4_SKY_PRETEST 0
+#define RT4_SKY_THRESHOLD 0
+#define RT4_BOUND_SKIP 0
+#endif
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -51,6 +59,11 @@ namespace {
 #define RT4_SKY_THRESHOLD 1
 #endif
 using WEntry = float;  // a {w, sqrt(1 - w*w)} table was 1 % faster on sphere, 6 % slower on room (rejected)
+#ifndef RT4_ABL_WLUT_STRIDE
+// A/B build only (RT4_ABL_WLUT_STRIDE=16: one entry per 64-B line, a 512 MiB table that cannot stay in
+// the 256 MiB Infinity Cache): where the gathers are served from (profiles/r03_ab.txt)
+#define RT4_ABL_WLUT_STRIDE 1
+#endif
 __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_ORDER_PREPASS
 #define RT4_ORDER_PREPASS 1  // longest-first tile order from a primary-ray pre-pass (rt4_tile_order_kernel)
@@ -185,8 +198,8 @@ __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, 
     float k = div_c(deviation, X->sun_ang), s = S->sun.sharpness;
     k = (s * s * k / (1.0f - s * k) + 1.0f) * (1.0f - k);
     float km = 1.0f - k;
-    return V3{fmaf_(S->sun.light[0], k, sky.x * km), fmaf_(S->sun.light[1], k, sky.y * km),
-              fmaf_(S->sun.light[2], k, sky.z * km)};
+    return V3{sfma_(S->sun.light[0], k, sky.x * km), sfma_(S->sun.light[1], k, sky.y * km),
+              sfma_(S->sun.light[2], k, sky.z * km)};
   }
   return sky;
 }
@@ -220,7 +233,7 @@ __device__ __forceinline__ V4 rand_drct(RngState& rng, const WEntry* __restrict_
     rng.iter += 0x79A010A9u;  // the w draw: its value was prefetched
     const WEntry e = w_pre;
 #else
-    const WEntry e = wlut[rand_bits(rng)];
+    const WEntry e = wlut[rand_bits(rng) * RT4_ABL_WLUT_STRIDE];
 #endif
     w = went_w(e);
     r = sqrt_(1.0f - w * w);
@@ -293,8 +306,8 @@ __device__ __forceinline__ V3 tone_map(const KernelArgs& a, V3 light) {
   const float ns = static_cast<float>(a.samples);
   light = V3{light.x / ns, light.y / ns, light.z / ns};
   const float k = a.k;
-  return V3{1.0f - 1.0f / fmaf_(k, light.x, 1.0f), 1.0f - 1.0f / fmaf_(k, light.y, 1.0f),
-            1.0f - 1.0f / fmaf_(k, light.z, 1.0f)};
+  return V3{1.0f - 1.0f / sfma_(k, light.x, 1.0f), 1.0f - 1.0f / sfma_(k, light.y, 1.0f),
+            1.0f - 1.0f / sfma_(k, light.z, 1.0f)};
 }
 
 // mix(old_frame, c, part), alpha 1 (shader.frag:527), per frame format (rt4.h rt4_frame_format; the
@@ -302,7 +315,7 @@ __device__ __forceinline__ V3 tone_map(const KernelArgs& a, V3 light) {
 // fold of pipelined frames, so both run the same ops.
 __device__ __forceinline__ float4 blend_f32(V3 c, float part, float4 old) {
   const float keep = 1.0f - part;
-  return make_float4(fmaf_(c.x, part, old.x * keep), fmaf_(c.y, part, old.y * keep), fmaf_(c.z, part, old.z * keep),
+  return make_float4(sfma_(c.x, part, old.x * keep), sfma_(c.y, part, old.y * keep), sfma_(c.z, part, old.z * keep),
                      1.0f);
 }
 __device__ __forceinline__ h4v blend_f16(V3 c, float part, h4v o) {
@@ -310,9 +323,9 @@ __device__ __forceinline__ h4v blend_f16(V3 c, float part, h4v o) {
   // the fp32 blend, THEN the rounding to half: the empty asm keeps the backend from fusing the fma
   // and the conversion into v_fma_mixlo_f16, which rounds once (differs from the contract in the
   // last half ulp: seen after 256 progressive frames of BASELINE config 5)
-  float b0 = fmaf_(c.x, part, static_cast<float>(o[0]) * keep);
-  float b1 = fmaf_(c.y, part, static_cast<float>(o[1]) * keep);
-  float b2 = fmaf_(c.z, part, static_cast<float>(o[2]) * keep);
+  float b0 = sfma_(c.x, part, static_cast<float>(o[0]) * keep);
+  float b1 = sfma_(c.y, part, static_cast<float>(o[1]) * keep);
+  float b2 = sfma_(c.z, part, static_cast<float>(o[2]) * keep);
   asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2));
   h4v v;
   v[0] = static_cast<_Float16>(b0);
@@ -325,7 +338,7 @@ __device__ __forceinline__ uint32_t blend_u8(V3 c, float part, uint32_t o) {
   const float keep = 1.0f - part;
   const float oc[3] = {static_cast<float>(o & 0xFFu) / 255.0f, static_cast<float>((o >> 8) & 0xFFu) / 255.0f,
                        static_cast<float>((o >> 16) & 0xFFu) / 255.0f};
-  const float nc[3] = {fmaf_(c.x, part, oc[0] * keep), fmaf_(c.y, part, oc[1] * keep), fmaf_(c.z, part, oc[2] * keep)};
+  const float nc[3] = {sfma_(c.x, part, oc[0] * keep), sfma_(c.y, part, oc[1] * keep), sfma_(c.z, part, oc[2] * keep)};
   uint32_t v = 0xFF000000u;
   for (int q = 0; q < 3; q++) v |= static_cast<uint32_t>(fminf(fmaxf(nc[q], 0.0f), 1.0f) * 255.0f + 0.5f) << (8 * q);
   return v;
@@ -555,7 +568,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       RT4_STAMP(t_ph);
       const V3 fl = final_light(S, X, ray.drct);
       RT4_ACC(2, t_ph);
-      acc = V3{fmaf_(T.x, fl.x, acc.x), fmaf_(T.y, fl.y, acc.y), fmaf_(T.z, fl.z, acc.z)};
+      acc = V3{sfma_(T.x, fl.x, acc.x), sfma_(T.y, fl.y, acc.y), sfma_(T.z, fl.z, acc.z)};
       return true;
     }
     RT4_LS(4);
@@ -566,7 +579,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
 #ifdef RT4_ABL_NOLUT  // ablation only (wrong images): the index arithmetic without the table gather
     if (LUT && diffuse) w_pre = WEntry{static_cast<float>(next_w_index(rng)) * 2.3841858e-7f - 1.0f};
 #else
-    if (LUT && diffuse) w_pre = wlut[next_w_index(rng)];  // in flight during resolve + shading
+    if (LUT && diffuse) w_pre = wlut[next_w_index(rng) * RT4_ABL_WLUT_STRIDE];  // in flight during resolve + shading
 #endif
 #endif
     RT4_STAMP(t_ph);
@@ -575,7 +588,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     V3 col;
     Finder<K>::material(S, P, h, glow, refl, col);
     RT4_ACC(3, t_ph);
-    acc = V3{fmaf_(col.x * glow, T.x, acc.x), fmaf_(col.y * glow, T.y, acc.y), fmaf_(col.z * glow, T.z, acc.z)};  // :481
+    acc = V3{sfma_(col.x * glow, T.x, acc.x), sfma_(col.y * glow, T.y, acc.y), sfma_(col.z * glow, T.z, acc.z)};  // :481
     T = V3{T.x * col.x, T.y * col.y, T.z * col.z};                                                                  // :482
     ray.point = add(ray.point, mad(ray.drct, h.dist, mul(h.norm, indent)));                                          // :485
     if (!diffuse) {  // :488 rand_outcome -> reflect
@@ -774,7 +787,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
               // a primary miss: every remaining sample is that same sky ray, acc = fma(T, sky, acc)
               // with T = 1, acc = 0 (:477-479), added to the sum sample by sample
               const V3 fl = final_light(S, X, ray.drct);
-              const V3 m{fmaf_(1.0f, fl.x, 0.0f), fmaf_(1.0f, fl.y, 0.0f), fmaf_(1.0f, fl.z, 0.0f)};
+              const V3 m{sfma_(1.0f, fl.x, 0.0f), sfma_(1.0f, fl.y, 0.0f), sfma_(1.0f, fl.z, 0.0f)};
               lp = make_float4(lp.x + m.x, lp.y + m.y, lp.z + m.z, lp.w);
               for (++s; s < NS; ++s) {
                 lp = make_float4(lp.x + m.x, lp.y + m.y, lp.z + m.z, lp.w);
@@ -827,7 +840,7 @@ __global__ void rt4_build_wlut_kernel(WEntry* __restrict__ lut) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= (1u << 23)) return;
   const float w = w_by_volume(__uint_as_float(m | 0x3F800000u) - 1.0f, nullptr);
-  lut[m] = w;
+  lut[m * RT4_ABL_WLUT_STRIDE] = w;
 }
 
 // Checks of the verified-divisor quotient div_c (rt4_fast.h) against the IEEE quotient x / b, one
@@ -1015,6 +1028,20 @@ __global__ void rt4_fold_frames_kernel(const KernelArgs a) {
     for (int f = 0; f < a.n_frames; f++) v = blend_f32(color(f), a.frame_part[f], v);
     *px = v;
   }
+}
+
+// The frame from the gathered band shards (rt4_bands_unpermute_device): one block per image row copies
+// the row from its place in the gather, in 16-B words when rows allow it, else 4-B words (every format's
+// pixel is a multiple of 4 B).
+template <typename W>
+__global__ void rt4_unpermute_kernel(const W* __restrict__ gathered, W* __restrict__ image, int32_t words_per_row,
+                                     int32_t world, int32_t band, int32_t rows_max) {
+  const int64_t y = blockIdx.x;
+  const int64_t b = y / band;
+  const int64_t src = (b % world) * rows_max + (b / world) * band + y % band;  // shard.py gather_index
+  const W* in = gathered + src * words_per_row;
+  W* out = image + y * words_per_row;
+  for (int32_t k = threadIdx.x; k < words_per_row; k += blockDim.x) out[k] = in[k];
 }
 
 // ---------------------------------------------------------------- kernel table
@@ -1565,7 +1592,7 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
     if (e == hipSuccess) e = hipDeviceSynchronize();
   }
   if (e == hipSuccess && (flags & RT4_FLAG_SAMPLER_LUT)) {
-    e = hipMalloc(&c->d_wlut, sizeof(WEntry) << 23);
+    e = hipMalloc(&c->d_wlut, (sizeof(WEntry) << 23) * RT4_ABL_WLUT_STRIDE);
     if (e == hipSuccess) {
       hipLaunchKernelGGL(rt4_build_wlut_kernel, dim3((1u << 23) / 256), dim3(256), 0, 0, c->d_wlut);
       e = hipGetLastError();
@@ -1642,7 +1669,6 @@ bool same_shared_uniforms(const rt4_uniforms& a, const rt4_uniforms& b) {
 // Frames pipelined in one launch (rt4_render_frames_device): per-frame seed and part of job 0.
 struct FramePlan {
   int32_t n;
-  int32_t cap;  // frames per launch for this frame size: the scratch is sized for cap, once
   const int32_t* seeds;
   const float* parts;
 };
@@ -1729,8 +1755,9 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // The tile order buffer is one per context: a launch on another stream than the previous one
   // waits for it (launches of one context run in submission order).
   if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(s, ctx->done, 0));
-  if (frames) {  // the frame colours of a pipelined launch: one scratch buffer per context, grown once
-    const size_t need = static_cast<size_t>(std::max(fp->n, fp->cap)) * static_cast<size_t>(a.jobs[0].reg.w) *
+  if (frames) {  // the frame colours of a pipelined launch: one scratch buffer per context, grown to the
+    // launch's frames (rt4_context_reserve_frames sizes it for a whole chunk ahead of time)
+    const size_t need = static_cast<size_t>(fp->n) * static_cast<size_t>(a.jobs[0].reg.w) *
                         static_cast<size_t>(a.jobs[0].reg.h) * sizeof(float4);
     if (ctx->fcolor_bytes < need) {
       HIP_TRY(hipStreamSynchronize(s));
@@ -1851,7 +1878,8 @@ int32_t rt4_context_frames_per_launch(const rt4_context* ctx, int32_t w, int32_t
 
 int rt4_context_reserve_frames(rt4_context* ctx, int32_t w, int32_t h, char* err, size_t errlen) {
   if (!ctx) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
-  const int32_t cap = frames_per_launch(w, h);
+  // the scene's own chunk size (a scene that runs frame by frame needs no scratch)
+  const int32_t cap = rt4_context_frames_per_launch(ctx, w, h);
   if (cap < 2) return RT4_OK;
   const size_t need = static_cast<size_t>(cap) * static_cast<size_t>(w) * static_cast<size_t>(h) * sizeof(float4);
   if (ctx->fcolor_bytes >= need) return RT4_OK;
@@ -1900,7 +1928,7 @@ int rt4_render_frames_device(rt4_context* ctx, const rt4_uniforms* u, int32_t n_
         seeds[f] = u[f0 + f].seed;
         parts[f] = u[f0 + f].part;
       }
-      const FramePlan fp{n, chunk, seeds, parts};
+      const FramePlan fp{n, seeds, parts};
       st = launch_jobs(ctx, &job, 1, format, d_counter, stream, err, errlen, &fp);
     }
     if (st != RT4_OK) return st;
@@ -1964,6 +1992,36 @@ int rt4_render_host_ex(rt4_context* ctx, const rt4_uniforms* u, const rt4_region
 int rt4_render_host(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* rgba,
                     int64_t row_stride_px, uint64_t* n_intersections, char* err, size_t errlen) {
   return rt4_render_host_ex(ctx, u, region, rgba, RT4_FRAME_RGBA32F, row_stride_px, n_intersections, err, errlen);
+}
+
+uint64_t rt4_context_frame_scratch_bytes(const rt4_context* ctx) { return ctx ? ctx->fcolor_bytes : 0u; }
+
+int rt4_bands_unpermute_device(const void* d_gathered, void* d_image, int32_t width, int32_t height, int32_t world,
+                               int32_t band, int32_t rows_max, int32_t format, void* stream, char* err, size_t errlen) {
+  if (!d_gathered || !d_image) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  const int32_t px = rt4_frame_format_bytes(format);
+  if (px == 0) return rt4_set_err(err, errlen, "unknown frame format %d", format), RT4_ERR_ARG;
+  if (width < 1 || height < 1 || world < 1 || band < 1 || rows_max < 1)
+    return rt4_set_err(err, errlen, "unpermute: width, height, world, band and rows_max must be >= 1"), RT4_ERR_ARG;
+  // every image row's source must lie inside the gather: the plan's rows_max (rt4_band_plan) or more
+  const int64_t need = rt4_band_rows_max(height, world, band);
+  if (static_cast<int64_t>(rows_max) < need)
+    return rt4_set_err(err, errlen, "unpermute: rows_max %d below the plan's %lld", rows_max, static_cast<long long>(need)),
+           RT4_ERR_ARG;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t row_bytes = static_cast<int64_t>(width) * px;
+  const bool wide = row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(d_gathered) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(d_image) % 16 == 0;
+  if (wide)
+    hipLaunchKernelGGL(rt4_unpermute_kernel<uint4>, dim3(static_cast<unsigned>(height)), dim3(256), 0, s,
+                       static_cast<const uint4*>(d_gathered), static_cast<uint4*>(d_image),
+                       static_cast<int32_t>(row_bytes / 16), world, band, rows_max);
+  else
+    hipLaunchKernelGGL(rt4_unpermute_kernel<uint32_t>, dim3(static_cast<unsigned>(height)), dim3(256), 0, s,
+                       static_cast<const uint32_t*>(d_gathered), static_cast<uint32_t*>(d_image),
+                       static_cast<int32_t>(row_bytes / 4), world, band, rows_max);
+  HIP_TRY(hipGetLastError());
+  return RT4_OK;
 }
 
 int rt4_debug_eval(rt4_context* ctx, int fn, const float* in, float* out, int32_t* aux, int64_t n, char* err,

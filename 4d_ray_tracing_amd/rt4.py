@@ -141,10 +141,11 @@ class SectionJob(Structure):  # rt4.h rt4_section_job
     _fields_ = [("u", Uniforms), ("region", Region), ("d_frame", c_void_p), ("row_stride_px", c_int64)]
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"librt4.so not found at {LIB_PATH}: build it first (python -c 'import __graft_entry__ as g; g.build()')")
-    lib = ctypes.CDLL(LIB_PATH)
+def _load(path=None):
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise ImportError(f"librt4.so not found at {path}: build it first (python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(path)
     E = [c_char_p, c_size_t]  # err, errlen
     sig = {
         "rt4_abi_version": ([], c_int),
@@ -198,6 +199,10 @@ def _load():
         "rt4_debug_verify_div": ([c_void_p, c_float, c_int32, POINTER(c_uint64)] + E, c_int),
         "rt4_context_evaluated": ([c_void_p, POINTER(c_uint64), c_int32] + E, c_int),
         "rt4_debug_sky_threshold": ([c_void_p, c_float, c_int32, POINTER(c_float)] + E, c_int),
+        "rt4_band_plan": ([c_int32, c_int32, c_int32, c_int32, c_int32, POINTER(Region), POINTER(c_int32)] + E, c_int),
+        "rt4_bands_unpermute_device": ([c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                        c_void_p] + E, c_int),
+        "rt4_context_frame_scratch_bytes": ([c_void_p], c_uint64),
     }
     tolerant = os.environ.get("RT4_AB_TOLERANT") == "1"  # tools/abtest.sh: older builds lack newer exports
     for name, (argtypes, restype) in sig.items():
@@ -210,6 +215,12 @@ def _load():
 
 
 lib = _load()
+
+
+def load_variant(path: str):
+    """Another build of librt4.so (e.g. the native-math diagnostic build, lib_native/librt4.so) with the
+    same C ABI, for Tracer(library=...): two builds side by side in one process."""
+    return _load(path)
 EXPORTED = (
     "rt4_abi_version rt4_build_info rt4_scene_desc_size rt4_uniforms_size rt4_properties_load rt4_properties_parse "
     "rt4_properties_free rt4_properties_has rt4_properties_get_string rt4_properties_get_int rt4_properties_get_uint "
@@ -219,7 +230,8 @@ EXPORTED = (
     "rt4_debug_eval rt4_debug_find_intersection rt4_context_kernel_shape rt4_debug_verify_sqrt "
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
-    "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch"
+    "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch "
+    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -396,6 +408,22 @@ def region(w: int, h: int, x0: int = 0, y0: int = 0, band_rows: int = 0, band_st
     return Region(x0, y0, w, h, band_rows, band_step)
 
 
+def band_plan(width: int, height: int, world: int, rank: int, band: int = 8):
+    """(region of `rank`, rows_max) of the C ABI's pixel-band plan (rt4_band_plan; shard.py make_plan)."""
+    reg, rows_max = Region(), c_int32()
+    err = _errbuf()
+    _check(lib.rt4_band_plan(width, height, world, band, rank, byref(reg), byref(rows_max), err, len(err)), err)
+    return reg, rows_max.value
+
+
+def bands_unpermute_device(gathered_ptr: int, image_ptr: int, width: int, height: int, world: int, rows_max: int,
+                           fmt: int = FRAME_RGBA32F, band: int = 8, stream: int = 0) -> None:
+    """The frame from world x rows_max gathered shard rows on the device (rt4_bands_unpermute_device)."""
+    err = _errbuf()
+    _check(lib.rt4_bands_unpermute_device(c_void_p(gathered_ptr), c_void_p(image_ptr), width, height, world, band,
+                                          rows_max, fmt, c_void_p(stream), err, len(err)), err)
+
+
 class Camera:
     """The reference's camera controller (src/controls.cpp) over rt4_camera: mouse/wheel rotation,
     WASD/Space/Shift/E/Q motion and per-frame uniforms (main.cpp:86-91)."""
@@ -457,7 +485,8 @@ def progressive_uniforms(base: Uniforms, frame_number: int) -> Uniforms:
 class Tracer:
     """Device context: scene on the device (+ optional sampler table) and the trace kernel."""
 
-    def __init__(self, device: int = 0, flags: int = 0, scene: Scene | None = None):
+    def __init__(self, device: int = 0, flags: int = 0, scene: Scene | None = None, library=None):
+        self._lib = library or lib  # library: load_variant(...) of another build (diagnostics)
         # librt4.so links the system HIP runtime; PyTorch-ROCm brings its own copy. In one process the
         # torch runtime must initialise first (torch.cuda reports no GPU when it comes second).
         torch = sys.modules.get("torch")
@@ -468,7 +497,7 @@ class Tracer:
                 pass
         h = c_void_p()
         err = _errbuf()
-        _check(lib.rt4_context_create(device, flags, byref(h), err, len(err)), err)
+        _check(self._lib.rt4_context_create(device, flags, byref(h), err, len(err)), err)
         self._h = h
         self.device = device
         if scene is not None:
@@ -476,27 +505,27 @@ class Tracer:
 
     def close(self):
         if getattr(self, "_h", None):
-            lib.rt4_context_destroy(self._h)
+            self._lib.rt4_context_destroy(self._h)
             self._h = None
 
     __del__ = close
 
     def set_scene(self, scene: Scene) -> None:
         err = _errbuf()
-        _check(lib.rt4_context_set_scene(self._h, byref(scene.desc), err, len(err)), err)
+        _check(self._lib.rt4_context_set_scene(self._h, byref(scene.desc), err, len(err)), err)
 
     def render_device(self, u: Uniforms, reg: Region, frame_ptr: int, row_stride_px: int, counter_ptr: int = 0,
                       stream: int = 0) -> None:
         """Asynchronous launch on `stream` into a device float4 framebuffer (e.g. a torch tensor's data_ptr())."""
         err = _errbuf()
-        _check(lib.rt4_render_device(self._h, byref(u), byref(reg), c_void_p(frame_ptr), row_stride_px,
+        _check(self._lib.rt4_render_device(self._h, byref(u), byref(reg), c_void_p(frame_ptr), row_stride_px,
                                      c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
 
     def render_device_ex(self, u: Uniforms, reg: Region, frame_ptr: int, fmt: int, row_stride_px: int,
                          counter_ptr: int = 0, stream: int = 0) -> None:
         """render_device into a device frame of any rt4_frame_format."""
         err = _errbuf()
-        _check(lib.rt4_render_device_ex(self._h, byref(u), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
+        _check(self._lib.rt4_render_device_ex(self._h, byref(u), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
                                         c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
 
     def render_frames_device(self, us, reg: Region, frame_ptr: int, fmt: int, row_stride_px: int,
@@ -505,17 +534,21 @@ class Tracer:
         result as render_device_ex(us[0]), render_device_ex(us[1]), ... in order."""
         arr = (Uniforms * len(us))(*us)
         err = _errbuf()
-        _check(lib.rt4_render_frames_device(self._h, arr, len(us), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
+        _check(self._lib.rt4_render_frames_device(self._h, arr, len(us), byref(reg), c_void_p(frame_ptr), fmt, row_stride_px,
                                             c_void_p(counter_ptr or None), c_void_p(stream or None), err, len(err)), err)
 
     def frames_per_launch(self, w: int, h: int) -> int:
         """Frames per pipelined launch for a w x h region with the current scene (1: frame by frame)."""
-        return int(lib.rt4_context_frames_per_launch(self._h, w, h))
+        return int(self._lib.rt4_context_frames_per_launch(self._h, w, h))
 
     def reserve_frames(self, w: int, h: int) -> None:
         """Allocate the frame-colour scratch of pipelined launches of a w x h region up front."""
         err = _errbuf()
-        _check(lib.rt4_context_reserve_frames(self._h, w, h, err, len(err)), err)
+        _check(self._lib.rt4_context_reserve_frames(self._h, w, h, err, len(err)), err)
+
+    def frame_scratch_bytes(self) -> int:
+        """Bytes of the context's frame-colour scratch (0: none allocated)."""
+        return int(self._lib.rt4_context_frame_scratch_bytes(self._h))
 
     def render_sections_device(self, jobs, fmt: int = FRAME_RGBA32F, counter_ptr: int = 0, stream: int = 0) -> None:
         """One launch over up to three images: jobs = [(uniforms, region, frame_ptr, row_stride_px), ...]."""
@@ -526,7 +559,7 @@ class Tracer:
             arr[q].d_frame = ptr
             arr[q].row_stride_px = stride
         err = _errbuf()
-        _check(lib.rt4_render_sections_device(self._h, arr, len(jobs), fmt, c_void_p(counter_ptr or None),
+        _check(self._lib.rt4_render_sections_device(self._h, arr, len(jobs), fmt, c_void_p(counter_ptr or None),
                                               c_void_p(stream or None), err, len(err)), err)
 
     def render_host_ex(self, u: Uniforms, reg: Region, frame, fmt: int, row_stride_px: int | None = None) -> int:
@@ -537,7 +570,7 @@ class Tracer:
         stride = row_stride_px if row_stride_px is not None else frame.shape[1]
         n = c_uint64()
         err = _errbuf()
-        _check(lib.rt4_render_host_ex(self._h, byref(u), byref(reg), c_void_p(frame.ctypes.data), fmt, stride,
+        _check(self._lib.rt4_render_host_ex(self._h, byref(u), byref(reg), c_void_p(frame.ctypes.data), fmt, stride,
                                       byref(n), err, len(err)), err)
         return n.value
 
@@ -549,14 +582,14 @@ class Tracer:
         stride = row_stride_px if row_stride_px is not None else frame.shape[1]
         n = c_uint64()
         err = _errbuf()
-        _check(lib.rt4_render_host(self._h, byref(u), byref(reg), c_void_p(frame.ctypes.data), stride, byref(n), err,
+        _check(self._lib.rt4_render_host(self._h, byref(u), byref(reg), c_void_p(frame.ctypes.data), stride, byref(n), err,
                                    len(err)), err)
         return n.value
 
     @property
     def kernel_shape(self) -> int:
         """Shape code of the trace kernel the scene runs on (rt4.h rt4_context_kernel_shape)."""
-        return lib.rt4_context_kernel_shape(self._h)
+        return self._lib.rt4_context_kernel_shape(self._h)
 
     def debug_eval(self, fn: int, x):
         import numpy as np
@@ -565,7 +598,7 @@ class Tracer:
         out = np.empty_like(x)
         aux = np.empty(x.shape, np.int32)
         err = _errbuf()
-        _check(lib.rt4_debug_eval(self._h, fn, c_void_p(x.ctypes.data), c_void_p(out.ctypes.data),
+        _check(self._lib.rt4_debug_eval(self._h, fn, c_void_p(x.ctypes.data), c_void_p(out.ctypes.data),
                                   c_void_p(aux.ctypes.data), x.size, err, len(err)), err)
         return out, aux
 
@@ -573,28 +606,28 @@ class Tracer:
         """Mismatches of the kernel's sqrt against IEEE sqrt over all 2^32 inputs (rt4.h)."""
         n = c_uint64(0)
         err = _errbuf()
-        _check(lib.rt4_debug_verify_sqrt(self._h, ctypes.byref(n), err, len(err)), err)
+        _check(self._lib.rt4_debug_verify_sqrt(self._h, ctypes.byref(n), err, len(err)), err)
         return n.value
 
     def evaluated(self, reset: bool = True) -> int:
         """find_intersection calls evaluated by RT4_FLAG_PRIMARY_REUSE launches since the last reset."""
         n = c_uint64(0)
         err = _errbuf()
-        _check(lib.rt4_context_evaluated(self._h, ctypes.byref(n), 1 if reset else 0, err, len(err)), err)
+        _check(self._lib.rt4_context_evaluated(self._h, ctypes.byref(n), 1 if reset else 0, err, len(err)), err)
         return n.value
 
     def debug_verify_div(self, b: float, full: bool = False) -> int:
         """Mismatches of the verified-divisor quotient x / b (reduced sweep, or all 2^32 numerators)."""
         n = c_uint64(0)
         err = _errbuf()
-        _check(lib.rt4_debug_verify_div(self._h, b, 1 if full else 0, ctypes.byref(n), err, len(err)), err)
+        _check(self._lib.rt4_debug_verify_div(self._h, b, 1 if full else 0, ctypes.byref(n), err, len(err)), err)
         return n.value
 
     def debug_sky_threshold(self, ang: float, full: bool = False) -> float:
         """Smallest float c with acos(c) < ang in the kernel's acos (NaN: none)."""
         c = c_float(0.0)
         err = _errbuf()
-        _check(lib.rt4_debug_sky_threshold(self._h, ang, 1 if full else 0, ctypes.byref(c), err, len(err)), err)
+        _check(self._lib.rt4_debug_sky_threshold(self._h, ang, 1 if full else 0, ctypes.byref(c), err, len(err)), err)
         return c.value
 
     def debug_find_intersection(self, rays):
@@ -604,6 +637,6 @@ class Tracer:
         out = np.empty((rays.shape[0], 8), np.float32)
         col = np.empty((rays.shape[0], 3), np.float32)
         err = _errbuf()
-        _check(lib.rt4_debug_find_intersection(self._h, c_void_p(rays.ctypes.data), c_void_p(out.ctypes.data),
+        _check(self._lib.rt4_debug_find_intersection(self._h, c_void_p(rays.ctypes.data), c_void_p(out.ctypes.data),
                                                c_void_p(col.ctypes.data), rays.shape[0], err, len(err)), err)
         return out, col

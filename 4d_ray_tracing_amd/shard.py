@@ -44,11 +44,6 @@ class BandPlan:
         """Rows of the largest shard: every rank's buffer (and the gather) has this many rows."""
         return max(1, max(self.rows(r) for r in range(self.world)))
 
-    # weak-scaling plans were sized by rows per rank; kept for callers that think in shards
-    @property
-    def rows_per_rank(self) -> int:
-        return self.rows_max
-
     def region_args(self, rank: int) -> dict:
         """Keyword arguments of rt4.region() for `rank` (local row i -> image row, include/rt4.h)."""
         if self.world == 1:
@@ -75,18 +70,20 @@ class BandPlan:
         return (b % self.world) * self.rows_max + (b // self.world) * self.band + y % self.band
 
 
-def make_plan(width: int, height: int, world: int, band: int = 8) -> BandPlan:
+def make_plan(width: int, *, height: int, world: int, band: int = 8) -> BandPlan:
     """Plan for a width x height frame over `world` ranks in bands of `band` rows. Any height >= 1
-    works; a rank gets no rows when world exceeds the band count."""
+    works; a rank gets no rows when world exceeds the band count. `height` is the WHOLE frame's rows
+    and keyword-only (round 1's make_plan took rows per rank there: an old positional call now fails
+    instead of silently planning an N-times-smaller frame)."""
     if world < 1 or height < 1 or width < 1 or band < 1:
         raise ValueError("width, height, world and band must be positive")
     return BandPlan(width, height, world, band)
 
 
-def weak_plan(width: int, rows_per_rank: int, world: int, band: int = 8) -> BandPlan:
+def weak_plan(width: int, *, rows_per_rank: int, world: int, band: int = 8) -> BandPlan:
     """Weak scaling: a frame of rows_per_rank * world rows, every rank the same number of rows when
     rows_per_rank is a multiple of band (otherwise the round-robin deal differs by at most one band)."""
-    return make_plan(width, rows_per_rank * world, world, band)
+    return make_plan(width, height=rows_per_rank * world, world=world, band=band)
 
 
 def unpermute(gathered, plan: BandPlan):

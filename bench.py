@@ -51,6 +51,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
+# the same peak in VALU lane-operations: 256 CUs x 4 SIMDs x 32 lanes per cycle (a wave64 VALU instruction
+# issues over 2 cycles, MI355X_MICROARCH.md) x 2.4 GHz; 157.3 TFLOP/s counts an fma as 2 FLOP
+PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
 METRIC = "ray-bounce intersections/s per GPU at 1080p·16spp·8bounce; %VALU roofline"
 
 CONFIGS = {  # BASELINE.json configs[1..4]
@@ -86,6 +89,7 @@ def parse_args(argv=None):
     p.add_argument("--primary-reuse", action="store_true",
                    help="RT4_FLAG_PRIMARY_REUSE for the main leg: value becomes reference-equivalent (labelled)")
     p.add_argument("--no-reuse-leg", action="store_true", help="skip the extra primary-reuse leg (N = 1)")
+    p.add_argument("--no-fbf-leg", action="store_true", help="skip the extra frame-by-frame leg (N = 1)")
     p.add_argument("--frame-by-frame", action="store_true",
                    help="one launch per frame (rt4_render_device_ex) instead of the pipelined frames of "
                         "rt4_render_frames_device (always so with a gather after every frame)")
@@ -199,9 +203,9 @@ def ops_per_unit(rt4, scene, u, width, height, threads):
     return ops / n, (ops - sampler_ops) / n, n
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same workload and kernel
-    version (profiles/**/pmc_*.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+def pmc_profile(config, frames_per_dispatch):
+    """The committed rocprofv3 PMC summary (profiles/**/pmc_*.json, tools/pmc_summary.py) of the same
+    workload, kernel version and launch shape (frames per pipelined dispatch) as this run, or None."""
     keys = ("scene", "width", "height_per_gpu", "spp", "bounces", "seed", "sampler_lut", "frame_format",
             "kernel_version", "progressive")
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_*.json"), recursive=True)):
@@ -210,8 +214,8 @@ def pmc_traffic(config):
         except (OSError, ValueError):
             continue
         pc = d.get("config", {})
-        if all(pc.get(k) == config.get(k) for k in keys) and d.get("derived", {}).get("hbm_bytes_per_launch"):
-            return d["derived"]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        if all(pc.get(k) == config.get(k) for k in keys) and d.get("frames_per_dispatch", 1) == frames_per_dispatch:
+            return d, os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -256,7 +260,8 @@ def main():
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
 
     strong = args.mode == "strong"
-    plan = shard.make_plan(args.width, args.height, world) if strong else shard.weak_plan(args.width, args.height, world)
+    plan = (shard.make_plan(args.width, height=args.height, world=world) if strong
+            else shard.weak_plan(args.width, rows_per_rank=args.height, world=world))
     scene = rt4.Scene.named(args.scene)
     flags = (0 if args.no_lut else rt4.FLAG_SAMPLER_LUT) | (rt4.FLAG_PRIMARY_REUSE if args.primary_reuse else 0)
 
@@ -396,6 +401,37 @@ def main():
     n_local = int(counter.item())
     evaluated = tracer.evaluated() if args.primary_reuse else None
 
+    # Extra leg (N = 1, pipelined headline): the same frames, one launch per frame (rt4_render_device_ex),
+    # as the reference draws one frame per loop iteration (main.cpp:93, windows.cpp:45): the per-launch
+    # drain is paid every frame. Reported beside the headline, never as value.
+    fbf_leg = None
+    if world == 1 and pipelined and not args.no_fbf_leg:
+        frame_no[0] = 0
+        frame.zero_()
+        for _ in range(args.warmup):
+            render()
+        torch.cuda.synchronize()
+        cnt_f = torch.zeros(1, dtype=torch.int64, device=dev)
+        f_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        f_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        tf0 = time.perf_counter()
+        for i in range(args.steps):
+            f_start[i].record(stream)
+            tracer.render_device_ex(uniforms(), reg, frame.data_ptr(), fmt, plan.width, cnt_f.data_ptr(), sptr)
+            f_end[i].record(stream)
+        torch.cuda.synchronize()
+        el_f = time.perf_counter() - tf0
+        n_f = int(cnt_f.item())
+        fbf_leg = {
+            "label": "one launch per frame (rt4_render_device_ex), as the reference draws one frame per loop "
+                     "iteration; same frames, same image and count as the pipelined headline",
+            "value": n_f / el_f, "unit": "ray-bounce intersections/s",
+            "ms_per_step": el_f / args.steps * 1e3,
+            "kernel_ms": sum(a.elapsed_time(b) for a, b in zip(f_start, f_end)) / args.steps,
+            "intersections_per_step": n_f / args.steps,
+        }
+
     # Extra leg (N = 1): the same frames with RT4_FLAG_PRIMARY_REUSE, reported beside the headline
     # (a reference-equivalent rate, with the evaluated count next to it).
     reuse_leg = None
@@ -482,7 +518,10 @@ def main():
             "accumulator": args.format,
             "data": "synthetic (fixed-seed procedural scene, no dataset)",
             "config": config,
+            "value_total": value,
             "value_per_gpu": value / world,
+            "value_note": "value = the whole job's intersections / the max-over-ranks time (bench contract; "
+                          "the driver derives scaling from it); the metric's per-GPU rate is value_per_gpu",
             "gather_ms": gather_ms,
             "intersections_per_step": n_total / args.steps,
             "nominal_bound_per_step": plan.width * plan.height * args.spp * (args.bounces + 1),
@@ -496,6 +535,8 @@ def main():
             line["evaluated_per_step"] = evaluated / args.steps if world == 1 else None
         if reuse_leg:
             line["primary_reuse_leg"] = reuse_leg
+        if fbf_leg:
+            line["frame_by_frame_leg"] = fbf_leg
         if strong:
             line["t1_ms"] = t1_ms if world > 1 else ms_per_step
             line["efficiency"] = (line["t1_ms"] / (world * ms_per_step)) if line["t1_ms"] else None
@@ -503,14 +544,19 @@ def main():
             opu, opu_exec, _ = ops_per_unit(rt4, scene, base, plan.width, plan.height, cpus["threads"])
             achieved = opu * units_per_launch / (kernel_ms * 1e-3) / 1e12
             achieved_exec = (opu if args.no_lut else opu_exec) * units_per_launch / (kernel_ms * 1e-3) / 1e12
-            traffic, src = pmc_traffic(config)
+            prof, src = pmc_profile(config, fpl)
+            der = prof.get("derived", {}) if prof else {}
+            cnt = prof.get("counters", {}) if prof else {}
             line["roofline"] = {
                 "bound": "valu",
                 "achieved": achieved,
                 "peak": PEAK_FP32_VALU_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_VALU_TFLOPS,
-                "traffic": traffic,
+                "traffic": der.get("hbm_bytes_per_launch"),
+                "achieved_kind": "reference-equivalent: the reference's fp32 ops per unit (oracle op count, fma = 2) "
+                                 "x units / kernel time; counts work the kernel skips exactly (tiger CSE, "
+                                 "bounding-ball skips, the sampler table), so it is not a hardware utilisation",
                 "ops_per_unit": opu,
                 "ops_per_unit_executed": opu if args.no_lut else opu_exec,
                 "frac_executed": achieved_exec / PEAK_FP32_VALU_TFLOPS,
@@ -519,10 +565,23 @@ def main():
                 "note": "fp32 ops (fma=2) per find_intersection+shading counted by the oracle on a row sample of "
                         "the frame; executed = without the w_by_volume Newton ops the sampler table replaces; "
                         "per launch = per frame (a pipelined launch holds frames_per_launch frames: its units, "
-                        "bytes and time are divided by them); see DESIGN.md §5",
+                        "bytes and time are divided by them); frac_counters = the VALU lane-operations the "
+                        "hardware counted (SQ_THREAD_CYCLES_VALU, same config, kernel version and launch shape) / "
+                        "(kernel time x 256 CU x 4 SIMD x 32 lanes x 2.4 GHz); see DESIGN.md §5",
             }
-            if src:
+            if prof and cnt.get("SQ_THREAD_CYCLES_VALU"):
+                lane_ops = cnt["SQ_THREAD_CYCLES_VALU"]  # per frame (pmc_summary divides a dispatch by its frames)
+                line["roofline"]["frac_counters"] = lane_ops / (kernel_ms * 1e-3) / PEAK_VALU_LANE_OPS
+                line["roofline"]["valu_lane_ops_per_frame"] = lane_ops
+                line["roofline"]["valu_lane_utilisation"] = der.get("valu_lane_utilisation")
+                line["roofline"]["valu_issue_frac"] = der.get("valu_issue_frac")
+                line["roofline"]["counters_source"] = src + (
+                    f" (rocprofv3 PMC, {prof.get('frames_per_dispatch', 1)} frames per dispatch, per frame; trace "
+                    f"{prof.get('avg_ns', 0) * 1e-6:.4f} ms per frame)")
+            if prof and der.get("hbm_bytes_per_launch"):
                 line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per frame)"
+            if prof and der.get("ea_read_latency_cycles"):
+                line["roofline"]["ea_read_latency_cycles"] = der["ea_read_latency_cycles"]
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(rt4, scene, base, plan.width, plan.rows_max, args.cpu_seconds, cpus)
         print(json.dumps(line), flush=True)

@@ -408,7 +408,29 @@ int rt4_context_reserve_frames(rt4_context* ctx, int32_t w, int32_t h, char* err
  * runs frame by frame: it measured slower pipelined. */
 int32_t rt4_context_frames_per_launch(const rt4_context* ctx, int32_t w, int32_t h);
 
+/* ---- multi-GPU pixel bands (replaces the one whole-texture draw of windows.cpp:45) ---
+ * A width x height frame is cut into bands of `band` rows (the last one may be short) dealt round-robin
+ * over `world` ranks, so every rank gets the same mix of cheap sky rows and expensive object rows. Every
+ * pixel is independent (shader.frag:104-108: the RNG depends only on the pixel, the seed and its own call
+ * counter), so the assembled image equals a one-GPU render bit for bit.
+ * rt4_band_plan: the region of `rank` (band layout of rt4_region; h = 0 when the rank owns no band) and
+ * rows_max, the rows of the largest shard (>= 1): every rank renders into a buffer of rows_max rows of
+ * width pixels, so one ncclGather of equal-size shards collects them (4d_ray_tracing_amd/shard.py
+ * make_plan is the same arithmetic). RT4_ERR_ARG for width, height, world or band < 1, or rank outside
+ * [0, world). */
+int rt4_band_plan(int32_t width, int32_t height, int32_t world, int32_t band, int32_t rank, rt4_region* region,
+                  int32_t* rows_max, char* err, size_t errlen);
+/* Assembles the frame on the root from the gathered shards: d_gathered holds world x rows_max rows of
+ * width pixels, rank-major (what ncclGather leaves on the root), d_image receives height rows of width
+ * pixels (row stride width); pixel size rt4_frame_format_bytes(format). Asynchronous on stream (a
+ * hipStream_t of the device that holds both buffers). */
+int rt4_bands_unpermute_device(const void* d_gathered, void* d_image, int32_t width, int32_t height, int32_t world,
+                               int32_t band, int32_t rows_max, int32_t format, void* stream, char* err, size_t errlen);
+
 /* ---- diagnostics (used by the parity tests; not on the render path) ------------------------- */
+/* Bytes of the context's frame-colour scratch for pipelined frames (0 before any pipelined launch or
+ * reservation; a scene that runs frame by frame never allocates it). */
+uint64_t rt4_context_frame_scratch_bytes(const rt4_context* ctx);
 enum rt4_eval_fn {
   RT4_EVAL_ACOS = 0, RT4_EVAL_ASIN = 1, RT4_EVAL_SIN = 2, RT4_EVAL_COS = 3,
   RT4_EVAL_VOLUME_BY_W = 4, /* shader.frag:136-138 */

@@ -32,6 +32,7 @@
 #include <cstdint>
 #include <cstring>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../include/rt4.h"
@@ -62,7 +63,17 @@ inline CF& operator+=(CF& a, CF b) { a = a + b; return a; }
 inline CF& operator*=(CF& a, CF b) { a = a * b; return a; }
 inline CF& operator/=(CF& a, CF b) { a = a / b; return a; }
 
+#ifdef RT4_NATIVE_MATH
+// Native-math mode (librt4_oracle_native.so): the shader's multiply-add forms as written,
+// a*b + c with two roundings, and the GLSL built-ins from glibc (acosf, asinf, sinf, cosf) instead of the
+// rt4m_* definitions. A sensitivity probe of the images to the built-ins' definition, which the
+// unrunnable GL reference leaves open; never the parity checker.
+inline float fma_(float a, float b, float c) { return a * b + c; }
+constexpr bool kNative = true;
+#else
 inline float fma_(float a, float b, float c) { return std::fmaf(a, b, c); }
+constexpr bool kNative = false;
+#endif
 inline float sqrt_(float a) { return std::sqrt(a); }
 inline float abs_(float a) { return std::fabs(a); }
 inline float rint_(float a) { return std::rint(a); }
@@ -90,6 +101,7 @@ template <class F> F rt4m_asin_core(F s, F z) {
 }
 
 template <class F> F rt4m_asin(F x) {
+  if constexpr (kNative && std::is_same<F, float>::value) return std::asin(x);
   F a = abs_(x);
   F r;
   if (a > F(0.5f)) {
@@ -103,6 +115,7 @@ template <class F> F rt4m_asin(F x) {
 }
 
 template <class F> F rt4m_acos(F x) {
+  if constexpr (kNative && std::is_same<F, float>::value) return std::acos(x);
   F a = abs_(x);
   if (a > F(0.5f)) {
     F z = F(0.5f) * (F(1.0f) - a);
@@ -133,11 +146,13 @@ template <class F> F rt4m_cos_kernel(F r) {
   return fma_(p, z * z, fma_(F(-0.5f), z, F(1.0f)));
 }
 template <class F> F rt4m_sin(F x) {
+  if constexpr (kNative && std::is_same<F, float>::value) return std::sin(x);
   F r; int q; rt4m_reduce(x, r, q);
   F s = rt4m_sin_kernel(r), c = rt4m_cos_kernel(r);
   switch (q) { case 0: return s; case 1: return c; case 2: return -s; default: return -c; }
 }
 template <class F> F rt4m_cos(F x) {
+  if constexpr (kNative && std::is_same<F, float>::value) return std::cos(x);
   F r; int q; rt4m_reduce(x, r, q);
   F s = rt4m_sin_kernel(r), c = rt4m_cos_kernel(r);
   switch (q) { case 0: return c; case 1: return -s; case 2: return -c; default: return s; }
@@ -485,19 +500,19 @@ void store_blend(void* px, int32_t fmt, const float c[3], float part) {
   const float keep = 1.0f - part;
   if (fmt == RT4_FRAME_RGBA16F) {
     uint16_t* h = static_cast<uint16_t*>(px);
-    for (int q = 0; q < 3; q++) h[q] = float_to_half(std::fma(c[q], part, half_to_float(h[q]) * keep));
+    for (int q = 0; q < 3; q++) h[q] = float_to_half(fma_(c[q], part, half_to_float(h[q]) * keep));
     h[3] = 0x3C00u;  // 1.0
   } else if (fmt == RT4_FRAME_RGBA8) {
     uint8_t* b = static_cast<uint8_t*>(px);
     for (int q = 0; q < 3; q++) {
       const float old = static_cast<float>(b[q]) / 255.0f;
-      const float v = std::fma(c[q], part, old * keep);
+      const float v = fma_(c[q], part, old * keep);
       b[q] = static_cast<uint8_t>(static_cast<uint32_t>(std::fmin(std::fmax(v, 0.0f), 1.0f) * 255.0f + 0.5f));
     }
     b[3] = 255;
   } else {
     float* f = static_cast<float*>(px);
-    for (int q = 0; q < 3; q++) f[q] = std::fma(c[q], part, f[q] * keep);
+    for (int q = 0; q < 3; q++) f[q] = fma_(c[q], part, f[q] * keep);
     f[3] = 1.0f;
   }
 }

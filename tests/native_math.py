@@ -1,0 +1,36 @@
+"""Native-math sensitivity report — TEST INFRASTRUCTURE ONLY.
+
+The reference is a GLSL 330 shader whose built-ins (acos, asin, sin, cos, and whether a*b + c is fused)
+are defined by whatever GL driver runs it; it cannot run here, so image parity is
+pinned to rt4's one deterministic definition. This module measures how far the images
+move when that definition is swapped for plain library built-ins with the shader's expressions unfused:
+  * CPU: oracle/build/librt4_oracle_native.so (glibc acosf/asinf/sinf/cosf) vs the deterministic oracle;
+  * GPU: lib_native/librt4.so (ocml, exact shortcuts compiled out) vs the deterministic kernel and vs the
+    native oracle (two different native libms, as two GL drivers would differ).
+Reported per BASELINE config 1-3 (SURVEY.md 8(c)'s fallback definition): the fraction of pixels whose
+RGB channels are all within 1e-4, the mean and max absolute channel error, the bit-identical pixel
+fraction and the intersection counts.
+"""
+import numpy as np
+
+CONFIGS = {  # BASELINE configs 1-3
+    1: ("sphere", 256, 256, 1, 2),
+    2: ("sphere", 1920, 1080, 16, 8),
+    3: ("hypercube", 1920, 1080, 16, 8),
+}
+
+
+def divergence(a, b, n_a=None, n_b=None):
+    """Pixel statistics of two RGBA float32 frames (RGB only)."""
+    e = np.abs(a[..., :3].astype(np.float64) - b[..., :3].astype(np.float64))
+    pix = e.max(axis=-1)
+    out = {
+        "pixels": int(pix.size),
+        "frac_within_1e-4": float((pix <= 1e-4).mean()),
+        "frac_bit_identical": float((pix == 0).mean()),
+        "mean_abs_error": float(e.mean()),
+        "max_abs_error": float(e.max()),
+    }
+    if n_a is not None:
+        out["intersections"] = [int(n_a), int(n_b)]
+    return out

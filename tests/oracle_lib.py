@@ -13,12 +13,14 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_PATH = os.path.join(ROOT, "oracle", "build", "librt4_oracle.so")
+# native-math mode: glibc built-ins and unfused shader forms; a sensitivity probe, never the checker
+NATIVE_PATH = os.path.join(ROOT, "oracle", "build", "librt4_oracle_native.so")
 
 
-def load():
-    if not os.path.exists(ORACLE_PATH):
-        raise FileNotFoundError(f"oracle not built: {ORACLE_PATH} (make -C oracle)")
-    lib = ctypes.CDLL(ORACLE_PATH)
+def load(path=ORACLE_PATH):
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"oracle not built: {path} (make -C oracle)")
+    lib = ctypes.CDLL(path)
     lib.oracle_hash.argtypes = [c_uint32]
     lib.oracle_hash.restype = c_uint32
     lib.oracle_scene_desc_size.restype = ctypes.c_size_t
@@ -34,10 +36,15 @@ def load():
 
 
 _lib = None
+_native = None
 
 
-def lib():
-    global _lib
+def lib(native=False):
+    global _lib, _native
+    if native:
+        if _native is None:
+            _native = load(NATIVE_PATH)
+        return _native
     if _lib is None:
         _lib = load()
     return _lib
@@ -53,11 +60,11 @@ def rand_first(W, H, seed, x, y, n):
     return out
 
 
-def eval_array(fn: int, x):
+def eval_array(fn: int, x, native=False):
     x = np.ascontiguousarray(x, dtype=np.float32)
     out = np.empty_like(x)
     aux = np.empty(x.shape, np.int32)
-    lib().oracle_eval_array(fn, x.ctypes.data, out.ctypes.data, aux.ctypes.data, x.size)
+    lib(native).oracle_eval_array(fn, x.ctypes.data, out.ctypes.data, aux.ctypes.data, x.size)
     return out, aux
 
 
@@ -71,8 +78,9 @@ def find_intersection(scene_desc, rays):
     return out, col
 
 
-def render(scene_desc, uniforms, reg, frame=None, threads=None, count_ops=False, pixel_counts=False):
-    """Renders `reg` into frame (h, w, 4) float32 (zeros if None). Returns (frame, n_inter, ops, counts)."""
+def render(scene_desc, uniforms, reg, frame=None, threads=None, count_ops=False, pixel_counts=False, native=False):
+    """Renders `reg` into frame (h, w, 4) float32 (zeros if None). Returns (frame, n_inter, ops, counts).
+    native=True: the native-math build (glibc built-ins, unfused), for the sensitivity report only."""
     h, w = reg.h, reg.w
     if frame is None:
         frame = np.zeros((h, w, 4), np.float32)
@@ -81,7 +89,7 @@ def render(scene_desc, uniforms, reg, frame=None, threads=None, count_ops=False,
     ops = c_uint64()
     counts = np.zeros((h, w), np.uint32) if pixel_counts else None
     threads = threads or os.cpu_count() or 1
-    st = lib().oracle_render(ctypes.addressof(scene_desc), ctypes.addressof(uniforms), ctypes.addressof(reg),
+    st = lib(native).oracle_render(ctypes.addressof(scene_desc), ctypes.addressof(uniforms), ctypes.addressof(reg),
                              frame.ctypes.data, frame.shape[1], threads, ctypes.byref(n), 1 if count_ops else 0,
                              ctypes.byref(ops), counts.ctypes.data if counts is not None else None)
     assert st == 0

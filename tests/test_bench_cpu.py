@@ -64,26 +64,32 @@ def test_executed_ops_drop_the_newton_loop(rt4):
     assert opu_exec == opu  # no hit, no diffuse bounce, no Newton loop
 
 
-def test_pmc_traffic_needs_the_same_workload_and_kernel(tmp_path, monkeypatch):
+def test_pmc_profile_needs_the_same_workload_kernel_and_shape(tmp_path, monkeypatch):
     prof = tmp_path / "profiles" / "rx"
     prof.mkdir(parents=True)
     cfg = {"scene": "sphere", "width": 1920, "height_per_gpu": 1080, "spp": 16, "bounces": 8, "seed": 12345,
            "sampler_lut": True, "frame_format": "f32", "kernel_version": "r02-test", "progressive": False}
-    (prof / "pmc_config2.json").write_text(json.dumps({"config": cfg, "derived": {"hbm_bytes_per_launch": 123.0}}))
+    (prof / "pmc_config2.json").write_text(json.dumps({"config": cfg, "frames_per_dispatch": 20,
+                                                       "derived": {"hbm_bytes_per_launch": 123.0}}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    assert bench.pmc_traffic(dict(cfg))[0] == 123.0
+    assert bench.pmc_profile(dict(cfg), 20)[0]["derived"]["hbm_bytes_per_launch"] == 123.0
+    assert bench.pmc_profile(dict(cfg), 5) == (None, None)  # another launch shape
     for k, v in (("kernel_version", "r02-other"), ("spp", 8), ("frame_format", "f16")):
-        assert bench.pmc_traffic(dict(cfg, **{k: v})) == (None, None)
+        assert bench.pmc_profile(dict(cfg, **{k: v}), 20) == (None, None)
 
 
 def test_committed_profiles_cover_every_config_of_the_current_kernel(rt4):
-    """The traffic figure of every config's bench line comes from a committed profile of the kernel
-    version librt4.so reports (profiles/r02_v*/pmc_config*.json)."""
+    """The traffic and frac_counters figures of every config's bench line come from a committed profile of
+    the kernel version librt4.so reports, taken at the bench's launch shape (profiles/r03_*/pmc_config*.json:
+    20 frames per pipelined dispatch, 32 for config 5, or one per dispatch where the scene runs frame by
+    frame)."""
     version = rt4.lib.rt4_build_info().decode().split()[2]
     for cfg in (2, 3, 4, 5):
         a = bench.parse_args(["--config", str(cfg)])
         config = {"scene": a.scene, "width": a.width, "height_per_gpu": a.height, "spp": a.spp, "bounces": a.bounces,
                   "seed": a.seed, "sampler_lut": True, "frame_format": a.format, "kernel_version": version,
                   "progressive": bool(a.progressive)}
-        traffic, src = bench.pmc_traffic(config)
-        assert traffic and traffic > 0, (cfg, version)
+        found = [bench.pmc_profile(config, f)[0] for f in (1, 20, 32)]
+        prof = next((p for p in found if p), None)
+        assert prof and prof["derived"].get("hbm_bytes_per_launch", 0) > 0, (cfg, version)
+        assert prof["counters"].get("SQ_THREAD_CYCLES_VALU", 0) > 0, (cfg, version)

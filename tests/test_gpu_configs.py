@@ -60,6 +60,36 @@ def test_full_frame_1080p_bitwise(rt4, oracle, name, config):
             assert n_eval == nc - 15 * 1920 * 1080, (n_eval, nc)
 
 
+@pytest.mark.parametrize("name,config", [("sphere", 2), ("hypercube", 3)])
+def test_bench_call_1080p_bitwise(rt4, oracle, name, config):
+    """The exact call the bench times for BASELINE config 2 / 3 (bench.py: 20 identical frames, part 1,
+    one rt4_render_frames_device call after rt4_context_reserve_frames, into a frame that holds the
+    warmup's image): the final frame equals the oracle's full 1920x1080 frame bit for bit and the
+    count is 20 x the oracle's. Reference: shader.frag:513-528, main.cpp:57-111."""
+    import torch
+
+    scene = rt4.Scene.named(name)
+    u = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
+    reg = rt4.region(1920, 1080)
+    c, nc, _, _ = oracle.render(scene.desc, u, reg, threads=THREADS)
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        s = torch.cuda.current_stream().cuda_stream
+        fr = torch.rand((1080, 1920, 4), dtype=torch.float32, device="cuda")  # old contents (part 1 replaces)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        t.reserve_frames(1920, 1080)
+        t.render_frames_device([u] * 3, reg, fr.data_ptr(), rt4.FRAME_RGBA32F, 1920, 0, s)  # the warmup
+        t.render_frames_device([u] * 20, reg, fr.data_ptr(), rt4.FRAME_RGBA32F, 1920, cnt.data_ptr(), s)
+        torch.cuda.synchronize()
+        assert t.frames_per_launch(1920, 1080) >= 20  # one pipelined launch holds all 20 frames
+        g = fr.cpu().numpy()
+    finally:
+        t.close()
+    assert int(cnt.item()) == 20 * nc
+    eq = bits_equal(g, c)
+    assert eq.all(), f"config {config}: {(~eq).sum()} of {eq.size} values differ"
+
+
 def fp16_blend_bound(n):
     """Worst-case |fp16 - fp32| accumulator difference after n progressive frames of values in [0, 1).
 

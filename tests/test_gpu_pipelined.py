@@ -10,27 +10,34 @@ pytestmark = pytest.mark.gpu
 DT = {0: np.float32, 1: np.float16, 2: np.uint8}
 
 
-def frames_both_ways(rt4, scene, us, reg, fmt, flags, init=None):
-    """(pipelined frame, its count), (sequential frame, its count) on the GPU."""
+def frames_both_ways(rt4, scene, us, reg, fmt, flags, init=None, stride=None, rows=None, reserve=None):
+    """(pipelined frame, its count), (sequential frame, its count) on the GPU. The frame buffer has
+    `rows` rows of `stride` pixels (default: the region's h and w); the region's pixels start at
+    column reg.x0 of that buffer, as rt4_render_device_ex addresses them (pixel (i, j) of the region
+    at i * stride + j of d_frame, which the caller offsets by x0)."""
     import torch
 
     tdt = {0: torch.float32, 1: torch.float16, 2: torch.uint8}[fmt]
+    stride = reg.w if stride is None else stride
+    rows = reg.h if rows is None else rows
+    reserve = (len(us) % 2 == 1) if reserve is None else reserve
     out = []
     for pipelined in (True, False):
         t = rt4.Tracer(device=0, flags=flags, scene=scene)
         try:
-            fr = torch.zeros((reg.h, reg.w, 4), dtype=tdt, device="cuda")
+            fr = torch.zeros((rows, stride, 4), dtype=tdt, device="cuda")
             if init is not None:
                 fr.copy_(torch.from_numpy(init))
+            base = fr.data_ptr() + reg.x0 * 4 * fr.element_size()
             cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
             s = torch.cuda.current_stream().cuda_stream
             if pipelined:
-                if len(us) % 2:  # odd frame counts also check that a reserved scratch is used as is
+                if reserve:  # odd frame counts also check that a reserved scratch is used as is
                     t.reserve_frames(reg.w, reg.h)
-                t.render_frames_device(us, reg, fr.data_ptr(), fmt, reg.w, cnt.data_ptr(), s)
+                t.render_frames_device(us, reg, base, fmt, stride, cnt.data_ptr(), s)
             else:
                 for u in us:
-                    t.render_device_ex(u, reg, fr.data_ptr(), fmt, reg.w, cnt.data_ptr(), s)
+                    t.render_device_ex(u, reg, base, fmt, stride, cnt.data_ptr(), s)
             torch.cuda.synchronize()
             out.append((fr.cpu().numpy(), int(cnt.item())))
         finally:
@@ -164,3 +171,59 @@ def test_cpp_host_pipelined_equals_frame_by_frame(rt4, tmp_path, fmt):
         count = [ln for ln in r.stdout.splitlines() if "intersections" in ln][0].split("intersections ")[1].split(",")[0]
         outs.append((open(pre + "_yxz.ppm", "rb").read(), count))
     assert outs[0] == outs[1]
+
+
+def test_padded_stride_and_x_offset(rt4):
+    """Pipelined frames into a sub-rectangle of a wider frame buffer (row_stride_px > w, x0 > 0): the
+    fold pass's own addressing (i * row_stride_px + j) against the sequential launches; the pixels
+    outside the region keep their old contents."""
+    scene = rt4.Scene.named("hypercube")
+    base = rt4.make_uniforms(100, 44, samples=2, reflections=4, seed=606)
+    us = [rt4.progressive_uniforms(base, n) for n in range(1, 6)]
+    reg = rt4.region(37, 44, x0=13)
+    for fmt in (0, 1, 2):
+        dt = DT[fmt]
+        rng = np.random.default_rng(fmt)
+        init = (rng.integers(0, 255, (44, 100, 4)).astype(np.uint8) if fmt == 2
+                else rng.random((44, 100, 4)).astype(dt))
+        (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, fmt, rt4.FLAG_SAMPLER_LUT, init=init, stride=100,
+                                            rows=44)
+        assert np_ == nq
+        assert same_bits(p, q), fmt
+        # columns outside [13, 50) are untouched, and the region's columns changed
+        assert same_bits(np.ascontiguousarray(p[:, :13]), np.ascontiguousarray(init[:, :13]))
+        assert same_bits(np.ascontiguousarray(p[:, 50:]), np.ascontiguousarray(init[:, 50:]))
+        assert not same_bits(np.ascontiguousarray(p[:, 13:50]), np.ascontiguousarray(init[:, 13:50]))
+
+
+@pytest.mark.parametrize("name", ["sphere", "hypercube"])
+def test_bench_shape_progressive_1080p(rt4, name):
+    """The bench's launch shape (BASELINE configs 2 / 3: 1920x1080, 16 spp, 8 bounces, 20 frames in one
+    rt4_render_frames_device call) with a different seed and part every frame, so that every frame's
+    slice of the multi-GB scratch and every 13-bit pixel field of the packed pixel word reaches the
+    image: against 20 frame-by-frame launches, bit for bit."""
+    scene = rt4.Scene.named(name)
+    base = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=12345)
+    us = [rt4.progressive_uniforms(base, n) for n in range(1, 21)]
+    reg = rt4.region(1920, 1080)
+    (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, rt4.FLAG_SAMPLER_LUT, reserve=True)
+    assert np_ == nq
+    assert same_bits(p, q)
+
+
+def test_config5_chunk_pipelined_equals_sequential(rt4):
+    """BASELINE config 5's launch shape: all_primitives at 3840x2160, 16 spp, 8 bounces, fp16 frame, 32
+    progressive frames (one full pipelined chunk at 4K: a 4.2 GB scratch) against 32 rt4_render_device_ex
+    launches, bit for bit, count included."""
+    scene = rt4.Scene.named("all_primitives")
+    base = rt4.make_uniforms(3840, 2160, samples=16, reflections=8, seed=12345)
+    us = [rt4.progressive_uniforms(base, n) for n in range(1, 33)]
+    reg = rt4.region(3840, 2160)
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+    try:
+        assert t.frames_per_launch(3840, 2160) == 32
+    finally:
+        t.close()
+    (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 1, rt4.FLAG_SAMPLER_LUT, reserve=True)
+    assert np_ == nq
+    assert same_bits(p, q)

@@ -1,0 +1,44 @@
+"""Native-math mode on the CPU: the oracle with glibc built-ins and unfused shader forms against the
+deterministic oracle on BASELINE configs 1-3 at their full shapes ("pixel
+fraction within 1e-4 plus mean error, reported"). A sensitivity report, not a parity test: the bounds
+below are what the measurement must stay under for the 1e-4 parity claim to mean anything beyond rt4's
+own definition of the built-ins. Reference built-ins: shader.frag:50 (acos), :129 (cos, sin), :137
+(acos), :211-217 (acos, sin, asin, cos)."""
+import importlib
+import json
+import os
+
+import pytest
+
+from native_math import CONFIGS, divergence
+
+THREADS = max(1, min(16, os.cpu_count() or 1))
+
+
+@pytest.mark.parametrize("config", [1, 2, 3])
+def test_native_libm_vs_deterministic_oracle(rt4, oracle, config):
+    name, W, H, spp, bounces = CONFIGS[config]
+    scene = rt4.Scene.named(name)
+    u = rt4.make_uniforms(W, H, samples=spp, reflections=bounces, seed=12345)
+    reg = rt4.region(W, H)
+    det, n_det, _, _ = oracle.render(scene.desc, u, reg, threads=THREADS)
+    nat, n_nat, _, _ = oracle.render(scene.desc, u, reg, threads=THREADS, native=True)
+    d = divergence(det, nat, n_det, n_nat)
+    print(f"config {config} native glibc vs deterministic: {json.dumps(d)}")
+    assert d["frac_within_1e-4"] >= 0.9999  # measured 1.0 / 0.99998 / 0.99998
+    assert d["mean_abs_error"] < 1e-6       # measured 1.3e-8 / 2.1e-8 / 3.1e-8
+    assert abs(n_nat - n_det) <= 1e-5 * n_det
+    assert (nat[..., 3] == 1.0).all() and (nat[..., :3] >= 0).all() and (nat[..., :3] < 1).all()
+
+
+def test_native_oracle_is_a_different_definition(rt4, oracle):
+    """The native build really swaps the built-ins: its acos differs from the deterministic one somewhere
+    on a dense sweep (else the report above would compare a definition with itself)."""
+    import numpy as np
+
+    x = np.linspace(-1.0, 1.0, 200001, dtype=np.float32)
+    for fn in (0, 1, 2, 3):  # RT4_EVAL_ACOS, ASIN, SIN, COS
+        det, _ = oracle.eval_array(fn, x)
+        nat, _ = oracle.eval_array(fn, x, native=True)
+        assert np.any(det.view(np.uint32) != nat.view(np.uint32)), fn
+        assert np.nanmax(np.abs(det.astype(np.float64) - nat)) < 1e-6, fn  # both ~1-2 ulp definitions

@@ -34,7 +34,7 @@ def _worker(rank, world, port, scene_name, width, height, out_dir):
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
     import oracle_lib
 
-    plan = shard.make_plan(width, height, world, band=8)
+    plan = shard.make_plan(width, height=height, world=world, band=8)
     scene = rt4.Scene.named(scene_name)
     u = rt4.make_uniforms(plan.width, plan.height, samples=1, reflections=2, seed=31337)
     reg = rt4.region(**plan.region_args(rank))
@@ -73,7 +73,7 @@ def test_banded_gather_equals_full_frame(tmp_path, world, height):
 @pytest.mark.parametrize("band", [1, 8, 16])
 def test_plan_rows_partition_the_frame(height, world, band):
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
-    plan = shard.make_plan(1920, height, world, band=band)
+    plan = shard.make_plan(1920, height=height, world=world, band=band)
     rows = [plan.rows(r) for r in range(world)]
     assert sum(rows) == height
     assert plan.rows_max == max(1, max(rows))
@@ -99,7 +99,7 @@ def test_4k_over_8_ranks_is_balanced():
     """BASELINE configs 4/5: 3840x2160 over 8 GPUs in 8-row bands -> 270 bands, 6 ranks x 34 + 2 x 33;
     the largest share is 0.7 % above the mean (the bound on strong-scaling efficiency from the split)."""
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
-    plan = shard.make_plan(3840, 2160, 8)
+    plan = shard.make_plan(3840, height=2160, world=8)
     assert [plan.bands(r) for r in range(8)] == [34] * 6 + [33] * 2
     assert plan.rows_max == 272
     assert plan.rows_max / (2160 / 8) < 1.01
@@ -107,8 +107,35 @@ def test_4k_over_8_ranks_is_balanced():
 
 def test_bad_plans_raise():
     shard = importlib.import_module("4d_ray_tracing_amd.shard")
-    for args in [(0, 10, 1), (10, 0, 1), (10, 10, 0)]:
+    for w, h, n in [(0, 10, 1), (10, 0, 1), (10, 10, 0)]:
         with pytest.raises(ValueError):
-            shard.make_plan(*args)
+            shard.make_plan(w, height=h, world=n)
     with pytest.raises(ValueError):
-        shard.make_plan(10, 10, 2, band=0)
+        shard.make_plan(10, height=10, world=2, band=0)
+    # height is keyword-only: round 1's positional (width, rows_per_rank, world) call fails loudly
+    with pytest.raises(TypeError):
+        shard.make_plan(1920, 1080, 8)
+
+
+@pytest.mark.parametrize("height", [1, 7, 8, 9, 17, 1080, 1081, 2160, 2161])
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("band", [1, 8, 16])
+def test_c_abi_band_plan_equals_shard_py(rt4, height, world, band):
+    """rt4_band_plan (the C++ multi-GPU host's plan, librt4.so) is shard.py's arithmetic: the same region
+    and rows_max for every rank (host code only, no GPU)."""
+    shard = importlib.import_module("4d_ray_tracing_amd.shard")
+    plan = shard.make_plan(640, height=height, world=world, band=band)
+    for rank in range(world):
+        reg, rows_max = rt4.band_plan(640, height, world, rank, band=band)
+        want = plan.region_args(rank)
+        got = dict(w=reg.w, h=reg.h, x0=reg.x0, y0=reg.y0, band_rows=reg.band_rows, band_step=reg.band_step)
+        assert got == want, (rank, got, want)
+        assert rows_max == plan.rows_max
+
+
+def test_c_abi_band_plan_rejects_bad_arguments(rt4):
+    for args in [(0, 10, 1, 0), (10, 0, 1, 0), (10, 10, 0, 0), (10, 10, 2, 2), (10, 10, 2, -1)]:
+        with pytest.raises(rt4.RT4Error):
+            rt4.band_plan(*args)
+    with pytest.raises(rt4.RT4Error):
+        rt4.band_plan(10, 10, 2, 0, band=0)

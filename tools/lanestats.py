@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Per-phase wave executions and lane occupancy from the -DRT4_LANESTATS diagnostic build.
-Usage: RT4_LIB=<lanestats .so> python tools/lanestats.py [scene] [spp] [bounces]"""
+
+Usage: RT4_LIB=<lanestats .so> python tools/lanestats.py [scene] [spp] [bounces] [W] [H] [frames] [mode]
+  mode: "pipelined" (frames in one rt4_render_frames_device call) or "fbf" (one launch per frame).
+The counters accumulate over every launch of the run (counter[16..] per phase, counter[40..41] exact
+sphere trips)."""
 import importlib
 import os
 import sys
@@ -10,19 +14,36 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 rt4 = importlib.import_module("4d_ray_tracing_amd")
-scene = sys.argv[1] if len(sys.argv) > 1 else "sphere"
-spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-bounces = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+a = sys.argv[1:]
+scene = a[0] if len(a) > 0 else "sphere"
+spp = int(a[1]) if len(a) > 1 else 16
+bounces = int(a[2]) if len(a) > 2 else 8
+W = int(a[3]) if len(a) > 3 else 1920
+H = int(a[4]) if len(a) > 4 else 1080
+frames = int(a[5]) if len(a) > 5 else 1
+mode = a[6] if len(a) > 6 else "fbf"
 t = rt4.Tracer(0, rt4.FLAG_SAMPLER_LUT | int(os.environ.get("RT4_EXTRA_FLAGS", "0"), 0), rt4.Scene.named(scene))
-u = rt4.make_uniforms(1920, 1080, samples=spp, reflections=bounces, seed=12345)
-frame = torch.zeros((1080, 1920, 4), device="cuda")
+u = rt4.make_uniforms(W, H, samples=spp, reflections=bounces, seed=12345)
+frame = torch.zeros((H, W, 4), device="cuda")
 cnt = torch.zeros(64, dtype=torch.int64, device="cuda")
-t.render_device(u, rt4.region(1920, 1080), frame.data_ptr(), 1920, cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
+s = torch.cuda.current_stream().cuda_stream
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+if mode == "pipelined" and frames > 1:
+    t.reserve_frames(W, H)
+ev0.record()
+if mode == "pipelined":
+    t.render_frames_device([u] * frames, rt4.region(W, H), frame.data_ptr(), 0, W, cnt.data_ptr(), s)
+else:
+    for _ in range(frames):
+        t.render_device(u, rt4.region(W, H), frame.data_ptr(), W, cnt.data_ptr(), s)
+ev1.record()
 torch.cuda.synchronize()
 c = cnt.cpu().tolist()
 names = ["loop iteration (active lanes)", "find (active)", "-", "miss", "hit", "reflect", "diffuse", "end of sample",
          "refill", "-"]
-print(f"{scene} spp={spp} bounces={bounces} intersections={c[0]}")
+print(f"{scene} {W}x{H} spp={spp} bounces={bounces} frames={frames} {mode} frames/launch="
+      f"{t.frames_per_launch(W, H) if mode == 'pipelined' else 1}: intersections={c[0]}, "
+      f"{ev0.elapsed_time(ev1) / frames:.3f} ms/frame (lanestats build)")
 for p, n in enumerate(names):
     e, l = c[16 + 2 * p], c[17 + 2 * p]
     if n == "-" or e == 0:
@@ -31,3 +52,4 @@ for p, n in enumerate(names):
 if c[40]:
     print(f"  {'exact sphere test (pending)':>30s}: {c[40]:12d} wave execs ({c[40] / max(c[16], 1):5.3f} per iteration), "
           f"{c[41] / c[40]:5.1f} lanes avg")
+print(f"  iterations per intersection: {c[16] / max(c[0], 1):.4f}")

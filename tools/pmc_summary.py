@@ -88,6 +88,9 @@ def main():
         # L2 misses sent to the fabric, and the part of them that reached DRAM (the rest: MALL hits)
         m["fabric_read_requests"] = c["TCC_EA0_RDREQ_sum"]
         m["dram_read_share"] = c["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, c["TCC_EA0_RDREQ_sum"])
+    if "TCC_EA0_RDREQ_LEVEL_sum" in c and "TCC_EA0_RDREQ_sum" in c:
+        # Little's law over the L2's fabric read interface (TCC cycles): the mean latency of an L2 miss
+        m["ea_read_latency_cycles"] = c["TCC_EA0_RDREQ_LEVEL_sum"] / max(1.0, c["TCC_EA0_RDREQ_sum"])
     out["derived"] = m
     for log in ("trace.log", os.path.join("trace", "..", "bench.log")):
         lp = os.path.join(d, log)
