@@ -549,6 +549,22 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
   return inter;
 }
 
+// The exact tests of a lane's pending spheres in index order (pass 2 of find_cand), from the cull's dots
+// or the centre.
+template <uint32_t SH>
+__device__ __forceinline__ Cand exact_pending(const SceneAux* __restrict__ X, const PrimEntry* P, const Ray& ray,
+                                              const SphereGeo& geo, uint32_t pend, Cand inter) {
+  while (pend) {
+    const int i = __builtin_ctz(pend);
+    pend &= pend - 1u;
+    if constexpr (geo_spheres<SH>() > 0)
+      inter = closest(sphere_exact_geo<SH>(X, P, geo, i), inter);
+    else
+      inter = closest(sphere_exact<SH>(X, P, ray, i), inter);
+  }
+  return inter;
+}
+
 template <uint32_t SH>
 __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
                                           const PrimEntry* P, const Ray& ray) {
@@ -558,6 +574,19 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
   SphereGeo geo;
   Cand inter = find_pre<SH>(S, X, ray, pend, &geo);
   if (K & K_SPHERES) {
+#ifdef RT4_LANESTATS  // diagnostic: histogram of the lanes with pending spheres per find (counter[42 + bucket]
+                      // wave events, counter[50 + bucket] lanes; buckets 1, 2, 3-4, 5-8, 9-16, 17-32, 33-64)
+    {
+      const unsigned long long pm = __ballot(pend != 0u);
+      const unsigned long long ex = __builtin_amdgcn_read_exec();
+      if (pm && rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+        const unsigned n = static_cast<unsigned>(__popcll(pm));
+        const unsigned bk = n <= 1u ? 0u : (n <= 2u ? 1u : (n <= 4u ? 2u : (n <= 8u ? 3u : (n <= 16u ? 4u : (n <= 32u ? 5u : 6u)))));
+        atomicAdd(rt4_ls_counter + 42 + bk, 1ull);
+        atomicAdd(rt4_ls_counter + 50 + bk, static_cast<unsigned long long>(n));
+      }
+    }
+#endif
     // Pass 2: each lane evaluates ITS pending spheres in index order, so a wave pays for
     // max-over-lanes(pending) exact evaluations instead of n_spheres.
     while (pend) {

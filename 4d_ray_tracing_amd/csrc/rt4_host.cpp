@@ -519,6 +519,98 @@ int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w
   return RT4_OK;
 }
 
+// ============================================================================ accumulator checkpoint
+namespace {
+constexpr char kAccMagic[8] = {'R', 'T', '4', 'A', 'C', 'C', '1', '\0'};
+struct AccHeader {  // the file's first 40 bytes (rt4.h), little-endian like every supported host
+  char magic[8];
+  int32_t version, w, h, format;
+  int64_t frames_done;
+  uint32_t seed, reserved;
+};
+static_assert(sizeof(AccHeader) == 40, "checkpoint header layout");
+
+int acc_read_header(std::FILE* f, const char* path, AccHeader& hd, char* err, size_t errlen) {
+  if (std::fread(&hd, 1, sizeof hd, f) != sizeof hd || std::memcmp(hd.magic, kAccMagic, sizeof kAccMagic) != 0)
+    return rt4_set_err(err, errlen, "%s is not an rt4 accumulator checkpoint", path), RT4_ERR_PARSE;
+  if (hd.version != RT4_ACCUM_VERSION)
+    return rt4_set_err(err, errlen, "%s: checkpoint version %d, expected %d", path, hd.version, RT4_ACCUM_VERSION),
+           RT4_ERR_PARSE;
+  if (hd.w <= 0 || hd.h <= 0 || rt4_frame_format_bytes(hd.format) == 0 || hd.frames_done < 0)
+    return rt4_set_err(err, errlen, "%s: bad checkpoint header", path), RT4_ERR_PARSE;
+  return RT4_OK;
+}
+}  // namespace
+
+int rt4_accum_save(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                   int64_t frames_done, uint32_t seed, char* err, size_t errlen) {
+  if (!path || !frame || w <= 0 || h <= 0 || row_stride_px < w || frames_done < 0)
+    return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
+  const int32_t px_bytes = rt4_frame_format_bytes(format);
+  if (px_bytes == 0) return rt4_set_err(err, errlen, "unknown frame format %d", format), RT4_ERR_ARG;
+  AccHeader hd{};
+  std::memcpy(hd.magic, kAccMagic, sizeof kAccMagic);
+  hd.version = RT4_ACCUM_VERSION;
+  hd.w = w;
+  hd.h = h;
+  hd.format = format;
+  hd.frames_done = frames_done;
+  hd.seed = seed;
+  std::FILE* f = std::fopen(path, "wb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s for writing", path), RT4_ERR_IO;
+  bool ok = std::fwrite(&hd, 1, sizeof hd, f) == sizeof hd;
+  const size_t row = static_cast<size_t>(w) * px_bytes;
+  for (int32_t i = 0; ok && i < h; i++)
+    ok = std::fwrite(static_cast<const unsigned char*>(frame) + static_cast<size_t>(i) * row_stride_px * px_bytes, 1,
+                     row, f) == row;
+  if (std::fclose(f) != 0) ok = false;
+  if (!ok) return rt4_set_err(err, errlen, "write failed: %s", path), RT4_ERR_IO;
+  return RT4_OK;
+}
+
+int rt4_accum_info(const char* path, int32_t* w, int32_t* h, int32_t* format, int64_t* frames_done, uint32_t* seed,
+                   char* err, size_t errlen) {
+  if (!path) return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
+  std::FILE* f = std::fopen(path, "rb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s", path), RT4_ERR_IO;
+  AccHeader hd{};
+  const int rc = acc_read_header(f, path, hd, err, errlen);
+  std::fclose(f);
+  if (rc != RT4_OK) return rc;
+  if (w) *w = hd.w;
+  if (h) *h = hd.h;
+  if (format) *format = hd.format;
+  if (frames_done) *frames_done = hd.frames_done;
+  if (seed) *seed = hd.seed;
+  return RT4_OK;
+}
+
+int rt4_accum_load(const char* path, void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                   int64_t* frames_done, uint32_t* seed, char* err, size_t errlen) {
+  if (!path || !frame || w <= 0 || h <= 0 || row_stride_px < w) return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
+  std::FILE* f = std::fopen(path, "rb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s", path), RT4_ERR_IO;
+  AccHeader hd{};
+  int rc = acc_read_header(f, path, hd, err, errlen);
+  if (rc == RT4_OK && (hd.w != w || hd.h != h || hd.format != format)) {
+    rt4_set_err(err, errlen, "%s holds a %dx%d frame of format %d, not %dx%d of format %d", path, hd.w, hd.h, hd.format,
+                w, h, format);
+    rc = RT4_ERR_ARG;
+  }
+  const int32_t px_bytes = rt4_frame_format_bytes(format);
+  const size_t row = static_cast<size_t>(w) * px_bytes;
+  for (int32_t i = 0; rc == RT4_OK && i < h; i++)
+    if (std::fread(static_cast<unsigned char*>(frame) + static_cast<size_t>(i) * row_stride_px * px_bytes, 1, row, f) != row) {
+      rt4_set_err(err, errlen, "%s: truncated checkpoint (row %d of %d)", path, i, h);
+      rc = RT4_ERR_PARSE;
+    }
+  std::fclose(f);
+  if (rc != RT4_OK) return rc;
+  if (frames_done) *frames_done = hd.frames_done;
+  if (seed) *seed = hd.seed;
+  return RT4_OK;
+}
+
 // ============================================================================ misc
 int rt4_abi_version(void) { return RT4_ABI_VERSION; }
 size_t rt4_scene_desc_size(void) { return sizeof(rt4_scene_desc); }

@@ -15,6 +15,8 @@
 //                   [-f f32|f16|rgba8] [--seed S] [-o prefix] [-d device] [--keys WASD...] [--move-seconds t]
 //                   [--frame-by-frame]  (one section and a resting camera: rt4_render_frames_device unless given)
 //                   [--gpus N [--band B]]  (one section, resting camera: bands over devices 0..N-1 + RCCL gather)
+//                   [--resume ckpt] [--checkpoint ckpt]  (one section: continue / save the progressive
+//                   accumulator, rt4_accum_load / rt4_accum_save; the reference has no counterpart)
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -210,6 +212,7 @@ int main(int argc, char** argv) {
   int gpus = 0, band = 8;
   uint32_t seed = 12345, keys = 0;
   float move_seconds = 0.0f;
+  std::string resume_path, checkpoint_path;
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -231,6 +234,8 @@ int main(int argc, char** argv) {
     else if (a == "--move-seconds") move_seconds = static_cast<float>(std::atof(next()));
     else if (a == "--gpus") gpus = std::atoi(next());
     else if (a == "--band") band = std::atoi(next());
+    else if (a == "--resume") resume_path = next();
+    else if (a == "--checkpoint") checkpoint_path = next();
     else die("unknown argument", a.c_str());
   }
   const int32_t format = fmt_name == "f16" ? RT4_FRAME_RGBA16F : fmt_name == "rgba8" ? RT4_FRAME_RGBA8 : RT4_FRAME_RGBA32F;
@@ -272,6 +277,20 @@ int main(int argc, char** argv) {
   rt4_camera cam;
   RT4_CHECK(rt4_camera_init(props, &cam, err, sizeof err));
 
+  if ((!resume_path.empty() || !checkpoint_path.empty()) && (three || gpus > 0))
+    die("--resume/--checkpoint", "need one section on one GPU");
+  // frames already blended into the accumulator (a resumed run continues at frame frames_done + 1)
+  int64_t frames_done = 0;
+  std::vector<unsigned char> resumed;
+  if (!resume_path.empty()) {
+    uint32_t ck_seed = 0;
+    resumed.resize(static_cast<size_t>(cw[0]) * ch[0] * rt4_frame_format_bytes(format));
+    RT4_CHECK(rt4_accum_load(resume_path.c_str(), resumed.data(), format, cw[0], ch[0], cw[0], &frames_done, &ck_seed, err,
+                             sizeof err));
+    if (ck_seed != seed) die("--resume", "the checkpoint was made with another --seed");
+    cam.frame_number = static_cast<uint32_t>(frames_done + 1);
+  }
+
   if (gpus > 0) {  // pixel bands over GPUs 0..gpus-1, one RCCL gather (one section, resting camera)
     if (three || (keys && move_seconds > 0.0f)) die("--gpus", "needs one section and a resting camera");
     if (frames < 1 || band < 1) die("--gpus", "frames and band must be >= 1");
@@ -308,6 +327,7 @@ int main(int argc, char** argv) {
     HIP_CHECK(hipMalloc(&d_frame[q], static_cast<size_t>(cw[q]) * ch[q] * px));
     HIP_CHECK(hipMemset(d_frame[q], 0, static_cast<size_t>(cw[q]) * ch[q] * px));  // cleared RenderTexture
   }
+  if (!resumed.empty()) HIP_CHECK(hipMemcpy(d_frame[0], resumed.data(), resumed.size(), hipMemcpyHostToDevice));
   unsigned long long* d_count = nullptr;
   HIP_CHECK(hipMalloc(&d_count, sizeof *d_count));
   HIP_CHECK(hipMemset(d_count, 0, sizeof *d_count));
@@ -326,8 +346,8 @@ int main(int argc, char** argv) {
       RT4_CHECK(rt4_context_reserve_frames(ctx, cw[0], ch[0], err, sizeof err));
     for (int n = 1; n <= frames; n++) {
       rt4_uniforms u;
-      RT4_CHECK(rt4_camera_frame_uniforms(&cam, &base[0], sections[0],
-                                          static_cast<int32_t>(seed ^ (static_cast<uint32_t>(n) * 0x9E3779B9u)), &u));
+      const uint32_t fn = static_cast<uint32_t>(frames_done + n);
+      RT4_CHECK(rt4_camera_frame_uniforms(&cam, &base[0], sections[0], static_cast<int32_t>(seed ^ (fn * 0x9E3779B9u)), &u));
       us.push_back(u);
     }
   }
@@ -338,7 +358,7 @@ int main(int argc, char** argv) {
                                        sizeof err));
   }
   for (int n = 1; n <= frames && !pipelined; n++) {
-    const int32_t s_n = static_cast<int32_t>(seed ^ (static_cast<uint32_t>(n) * 0x9E3779B9u));
+    const int32_t s_n = static_cast<int32_t>(seed ^ (static_cast<uint32_t>(frames_done + n) * 0x9E3779B9u));
     rt4_section_job jobs[3];
     const uint32_t frame_number = cam.frame_number;
     for (int q = 0; q < n_img; q++) {
@@ -365,6 +385,12 @@ int main(int argc, char** argv) {
     const std::string path = out + "_" + names[q] + ".ppm";
     RT4_CHECK(rt4_write_ppm(path.c_str(), host.data(), format, cw[q], ch[q], cw[q], err, sizeof err));
     std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[q], ch[q]);
+    if (q == 0 && !checkpoint_path.empty()) {
+      // frames_done counts camera-resting frames only: a moving camera restarts the blend (frame_number 1)
+      RT4_CHECK(rt4_accum_save(checkpoint_path.c_str(), host.data(), format, cw[0], ch[0], cw[0],
+                               static_cast<int64_t>(cam.frame_number) - 1, seed, err, sizeof err));
+      std::printf("checkpoint %s (%lld frames)\n", checkpoint_path.c_str(), static_cast<long long>(cam.frame_number) - 1);
+    }
   }
   std::printf("frames %d, images %d, intersections %llu, %.3f ms/frame, %.3e intersections/s\n", frames, n_img,
               count, ms / frames, static_cast<double>(count) / (ms * 1e-3));

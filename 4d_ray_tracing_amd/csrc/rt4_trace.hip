@@ -49,6 +49,15 @@ namespace {
 #ifndef RT4_REFILL_MIN
 #define RT4_REFILL_MIN 1  // refill as soon as one lane is idle (A/B: 8 -> 1 is +4.5 % sphere, +6 % hypercube, +4 % tiger)
 #endif
+#ifndef RT4_PHASE_REFILL
+// Phase-aligned refill: idle lanes of a wave that still has active lanes are refilled
+// only in an iteration where some active lane starts a sample (b == 0), so a new pixel's bounces run in
+// phase with the wave's other paths. In a closed scene (config 4's mirror room: every path runs all
+// R + 1 bounces) the lanes of a wave then stay in lockstep, bounce for bounce, instead of drifting apart
+// with every early miss; in open scenes some lane starts a sample in almost every iteration, so the
+// refill stays immediate. 0 = refill as soon as REFILL_MIN lanes are idle (A/B knob).
+#define RT4_PHASE_REFILL 1
+#endif
 #ifndef RT4_LUT_PREFETCH
 // When the sampler-table entry of a possible diffuse bounce is fetched: 2 = at a hit, in flight
 // during resolve + shading; 0 = in rand_drct. Measured alternatives, all slower (profiles/r01_ab.txt):
@@ -76,6 +85,12 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 // slower: sphere -13 %, room -7 %, all_primitives -21 % (profiles/r02_ab.txt): the four waves must
 // iterate in step, and two barriers per iteration cost more than the denser tests save. Off.
 #define RT4_POOL_SPHERES 0
+#endif
+#ifndef RT4_DEFER_EXACT
+#define RT4_DEFER_EXACT 0
+#endif
+#ifndef RT4_DEFER_WAIT
+#define RT4_DEFER_WAIT 2
 #endif
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
@@ -429,6 +444,10 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   __shared__ uint4 lds_pn4;                            // pairs of each wave | busy << 31, one word per wave
   uint32_t* const lds_pn = reinterpret_cast<uint32_t*>(&lds_pn4);
   const unsigned wave = threadIdx.x >> 6;
+  // Deferred exact sphere tests (A/B knob RT4_DEFER_EXACT = the wave's pending-lane threshold, 0 = off;
+  // RT4_DEFER_WAIT = the most iterations a parked lane waits): DESIGN.md §9, profiles/r03_ab.txt
+  constexpr bool DEFER = RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && sh_count(K, 2) != 0;
+  int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
 
   bool exhausted = false;
   bool active = false, pending = false;
@@ -610,7 +629,13 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     RT4_STAMP(t_ph);
     if (!exhausted) {
       const unsigned long long idle = __ballot(!active);
-      if (static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN) {
+      bool refill = static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN;
+      // phase-aligned: with active lanes left, wait (at most R + 1 iterations) for one of them to start
+      // a sample; every active lane finishes a sample within R + 1 iterations, so the wait is bounded.
+      // Not with primary reuse: there a sample's bounce 0 is shaded in the iteration that ends the previous
+      // sample, so a starting sample is at b == 1 at the top of the loop.
+      if (RT4_PHASE_REFILL && !REUSE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
+      if (refill) {
         RT4_LS(8);
         retire();
         const unsigned rank =
@@ -657,6 +682,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     ls[1] += __popcll(__ballot(active));
 #endif
     typename Finder<K>::R c{};
+    bool parked = false;  // DEFER: the lane's exact sphere tests wait for a later iteration
     if constexpr (POOL) {
       // find part 1 + publish; barrier; pooled exact tests; barrier; combine (find part 2 below)
       RT4_STAMP(t_ph);
@@ -726,6 +752,28 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
         c = find_rest<K>(S, X, P, ray, inter);
       }
       RT4_ACC(1, t_ph);
+    } else if constexpr (DEFER) {
+      // find in two parts with the exact sphere tests deferred: lanes whose cull leaves
+      // pending spheres park (no shading, no count) until enough lanes of the wave are pending; a parked
+      // lane redoes the cull next iteration (same ray, same bits) instead of keeping its state
+      if (!__any(active)) {
+        if (exhausted) break;
+        continue;
+      }
+      uint32_t pend = 0;
+      SphereGeo geo;
+      Cand inter = no_cand();
+      if (active) inter = find_pre<K>(S, X, ray, pend, &geo);
+      const unsigned long long pm = __ballot(pend != 0u);
+      const bool run = pm != 0ull && (static_cast<unsigned>(__popcll(pm)) >= static_cast<unsigned>(RT4_DEFER_EXACT) ||
+                                      defer_age >= RT4_DEFER_WAIT || pm == __ballot(active));
+      if (pm != 0ull && !run) {
+        parked = pend != 0u;
+        ++defer_age;
+      } else {
+        defer_age = 0;
+      }
+      if (active && !parked) c = find_rest<K>(S, X, P, ray, exact_pending<K>(X, P, ray, geo, pend, inter));
     } else {
       if (!__any(active)) {
         if (exhausted) break;
@@ -737,7 +785,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
         RT4_ACC(1, t_ph);
       }
     }
-    if (active) {
+    if (active && !parked) {
       RT4_LS(1);
       ++n_inter;
       ++n_eval;

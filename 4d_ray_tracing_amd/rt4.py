@@ -203,6 +203,11 @@ def _load(path=None):
         "rt4_bands_unpermute_device": ([c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                         c_void_p] + E, c_int),
         "rt4_context_frame_scratch_bytes": ([c_void_p], c_uint64),
+        "rt4_accum_save": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64, c_int64, c_uint32] + E, c_int),
+        "rt4_accum_info": ([c_char_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int64),
+                            POINTER(c_uint32)] + E, c_int),
+        "rt4_accum_load": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64, POINTER(c_int64), POINTER(c_uint32)]
+                           + E, c_int),
     }
     tolerant = os.environ.get("RT4_AB_TOLERANT") == "1"  # tools/abtest.sh: older builds lack newer exports
     for name, (argtypes, restype) in sig.items():
@@ -231,7 +236,7 @@ EXPORTED = (
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
     "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch "
-    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes"
+    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_accum_save rt4_accum_info rt4_accum_load"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -465,6 +470,43 @@ def write_ppm(path: str, frame, fmt: int | None = None) -> None:
     h, w = frame.shape[:2]
     err = _errbuf()
     _check(lib.rt4_write_ppm(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, err, len(err)), err)
+
+
+def accum_save(path: str, frame, frames_done: int, seed: int, fmt: int | None = None) -> None:
+    """Checkpoint of a progressive accumulator (rt4_accum_save): the (h, w, 4) host frame and the number of
+    frames already blended into it, with the base seed of its rt4_progressive_uniforms."""
+    import numpy as np
+
+    frame = np.ascontiguousarray(frame)
+    if fmt is None:
+        fmt = {np.dtype("float32"): FRAME_RGBA32F, np.dtype("float16"): FRAME_RGBA16F,
+               np.dtype("uint8"): FRAME_RGBA8}[frame.dtype]
+    h, w = frame.shape[:2]
+    err = _errbuf()
+    _check(lib.rt4_accum_save(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, frames_done,
+                              seed & 0xFFFFFFFF, err, len(err)), err)
+
+
+def accum_info(path: str) -> dict:
+    """The checkpoint's header (rt4_accum_info): w, h, format, frames_done, seed."""
+    w, h, f, n, sd = c_int32(), c_int32(), c_int32(), c_int64(), c_uint32()
+    err = _errbuf()
+    _check(lib.rt4_accum_info(os.fsencode(path), byref(w), byref(h), byref(f), byref(n), byref(sd), err, len(err)), err)
+    return {"w": w.value, "h": h.value, "format": f.value, "frames_done": n.value, "seed": sd.value}
+
+
+def accum_load(path: str):
+    """(frame, frames_done, seed) from a checkpoint (rt4_accum_load); frame is an (h, w, 4) numpy array of the
+    checkpoint's format."""
+    import numpy as np
+
+    info = accum_info(path)
+    frame = np.empty((info["h"], info["w"], 4), dtype=FRAME_NUMPY[info["format"]])
+    n, sd = c_int64(), c_uint32()
+    err = _errbuf()
+    _check(lib.rt4_accum_load(os.fsencode(path), c_void_p(frame.ctypes.data), info["format"], info["w"], info["h"],
+                              info["w"], byref(n), byref(sd), err, len(err)), err)
+    return frame, n.value, sd.value
 
 
 def frame_format_bytes(fmt: int) -> int:

@@ -275,6 +275,25 @@ int rt4_camera_frame_uniforms(rt4_camera* cam, const rt4_uniforms* base, int sec
 int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
                   char* err, size_t errlen);
 
+/* ---- accumulator checkpoint / resume (no reference counterpart) ----------------
+ * The reference keeps the progressive average only in the window's texture: old_frame is blended with
+ * part = 1/frameNumber (main.cpp:86-91) and restarts at frameNumber = 1 when the camera moves
+ * (controls.cpp:132,181,190). A checkpoint is that texture in its rt4_frame_format plus the number of
+ * frames already blended and the base seed, so a resumed run (frames frames_done + 1, ... through
+ * rt4_progressive_uniforms) continues the same blend bit for bit.
+ * File (little-endian): "RT4ACC1\0", int32 version (1), w, h, format, int64 frames_done, uint32 seed,
+ * uint32 reserved (0), then h rows of w pixels, rows top first, no padding. */
+#define RT4_ACCUM_VERSION 1
+int rt4_accum_save(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                   int64_t frames_done, uint32_t seed, char* err, size_t errlen);
+/* Header only: any output pointer may be null. RT4_ERR_PARSE for a file that is not a checkpoint. */
+int rt4_accum_info(const char* path, int32_t* w, int32_t* h, int32_t* format, int64_t* frames_done, uint32_t* seed,
+                   char* err, size_t errlen);
+/* Reads the pixels into a host frame of the checkpoint's w, h and format (RT4_ERR_ARG if the caller's
+ * differ); the header fields as rt4_accum_info. */
+int rt4_accum_load(const char* path, void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                   int64_t* frames_done, uint32_t* seed, char* err, size_t errlen);
+
 /* ---- scenes ------------------------------------------------------------------------------- */
 /* Accepts a scene snippet (scenes/<name>.frag) or a whole shader.frag; UTF-8 paths. */
 int rt4_scene_load_frag(const char* path, rt4_scene_desc* out, char* err, size_t errlen);

@@ -297,3 +297,65 @@ def test_queue_words_across_many_launches(rt4, oracle):
         assert (fr.cpu().numpy().view(np.uint32) == c.view(np.uint32)).all()
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("fmt", ["f32", "f16"])
+def test_progressive_resume_bitwise(rt4, tmp_path, fmt):
+    """Accumulator checkpoint / resume (rt4_accum_save / rt4_accum_load): 5 progressive frames, a checkpoint,
+    a fresh context and 4 more frames from the loaded accumulator equal 9 frames in one run, bit for bit
+    (the blend part = 1/n and seed_n continue from the checkpoint's frame count; main.cpp:86-91)."""
+    import torch
+
+    f = FORMATS[fmt]
+    tdt = {0: torch.float32, 1: torch.float16}[f]
+    W, H = 96, 64
+    base = rt4.make_uniforms(W, H, samples=3, reflections=5, seed=31337)
+    reg = rt4.region(W, H)
+    scene = rt4.Scene.named("all_primitives")
+
+    def run(frame, first, last):
+        t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
+        try:
+            t.render_frames_device([rt4.progressive_uniforms(base, n) for n in range(first, last + 1)], reg,
+                                   frame.data_ptr(), f, W, 0, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            t.close()
+
+    whole = torch.zeros((H, W, 4), dtype=tdt, device="cuda")
+    run(whole, 1, 9)
+    part = torch.zeros((H, W, 4), dtype=tdt, device="cuda")
+    run(part, 1, 5)
+    path = str(tmp_path / "acc.rt4")
+    rt4.accum_save(path, part.cpu().numpy(), frames_done=5, seed=31337, fmt=f)
+    host, done, seed = rt4.accum_load(path)
+    assert (done, seed) == (5, 31337)
+    resumed = torch.from_numpy(host).cuda()
+    run(resumed, done + 1, 9)
+    eq = bits_equal(resumed.cpu().numpy(), whole.cpu().numpy())
+    assert eq.all(), f"{(~eq).sum()} values differ"
+
+
+def test_cpp_host_program_resume(rt4, tmp_path):
+    """rt4_render --checkpoint / --resume: 3 frames, checkpoint, 3 more resumed frames write the same PPM
+    (and the same checkpoint) as 6 frames in one run."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(rt4.LIB_PATH), "rt4_render")
+    props = os.path.join(os.path.dirname(rt4.LIB_PATH), "..", "..", "properties.txt")
+    common = [exe, "-p", props, "-s", "sphere", "-W", "120", "-H", "80", "--seed", "99", "-f", "f32"]
+
+    def go(*args):
+        r = subprocess.run(common + list(args), capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+
+    go("-n", "6", "-o", str(tmp_path / "whole"), "--checkpoint", str(tmp_path / "whole.rt4"))
+    go("-n", "3", "-o", str(tmp_path / "a"), "--checkpoint", str(tmp_path / "a.rt4"))
+    assert rt4.accum_info(str(tmp_path / "a.rt4"))["frames_done"] == 3
+    go("-n", "3", "-o", str(tmp_path / "b"), "--resume", str(tmp_path / "a.rt4"), "--checkpoint", str(tmp_path / "b.rt4"))
+    assert (tmp_path / "b_yxz.ppm").read_bytes() == (tmp_path / "whole_yxz.ppm").read_bytes()
+    assert (tmp_path / "b.rt4").read_bytes() == (tmp_path / "whole.rt4").read_bytes()
+    r = subprocess.run(common[:-4] + ["--seed", "100", "-n", "1", "-o", str(tmp_path / "c"), "--resume",
+                                      str(tmp_path / "a.rt4")], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "another --seed" in r.stderr

@@ -9,24 +9,29 @@ VDIR=$ROOT/4d_ray_tracing_amd/lib/variants
 cmd=${1:-}; shift || true
 if [ "$cmd" = build ]; then
   rm -rf "$VDIR"; mkdir -p "$VDIR"
-  for spec in "$@"; do
+  build_one() {
+    local spec=$1 name rev flags tmpo tmp
     name=${spec%%=*}; rev=${spec#*=}
     flags=""
     case "$rev" in WORKTREE:*) flags=${rev#WORKTREE:}; rev=WORKTREE;; esac
     if [ "$rev" = WORKTREE ]; then
       tmpo=$(mktemp -d)
-      make -C "$ROOT/4d_ray_tracing_amd/csrc" -s OUT="$tmpo" EXTRA="$flags" >/dev/null
+      make -C "$ROOT/4d_ray_tracing_amd/csrc" -s OUT="$tmpo" EXTRA="$flags" "$tmpo/librt4.so" >/dev/null
       cp "$tmpo/librt4.so" "$VDIR/$name.so"
       rm -rf "$tmpo"
     else
       tmp=$(mktemp -d)
       git -C "$ROOT" archive "$rev" 4d_ray_tracing_amd/csrc include | tar -x -C "$tmp"
-      make -C "$tmp/4d_ray_tracing_amd/csrc" -s OUT="$tmp/lib" >/dev/null
+      make -C "$tmp/4d_ray_tracing_amd/csrc" -s OUT="$tmp/lib" "$tmp/lib/librt4.so" >/dev/null
       cp "$tmp/lib/librt4.so" "$VDIR/$name.so"
       rm -rf "$tmp"
     fi
     echo "built $name ($rev)"
-  done
+  }
+  # the variants build in parallel (one hipcc each; 8 host CPUs)
+  pids=()
+  for spec in "$@"; do build_one "$spec" & pids+=($!); done
+  for p in "${pids[@]}"; do wait "$p" || exit 1; done
 elif [ "$cmd" = run ]; then
   rounds=${1:-2}; shift || true
   args=${*:-"--steps 30 --warmup 3 --no-cpu-baseline"}

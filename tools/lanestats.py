@@ -52,4 +52,10 @@ for p, n in enumerate(names):
 if c[40]:
     print(f"  {'exact sphere test (pending)':>30s}: {c[40]:12d} wave execs ({c[40] / max(c[16], 1):5.3f} per iteration), "
           f"{c[41] / c[40]:5.1f} lanes avg")
+if any(c[42:49]):
+    tot = sum(c[42:49])
+    print("  finds with pending spheres, by lanes pending (wave events share, lanes avg):")
+    for k, lab in enumerate(["1", "2", "3-4", "5-8", "9-16", "17-32", "33-64"]):
+        if c[42 + k]:
+            print(f"    {lab:>6s}: {c[42 + k] / tot:6.3f}  {c[50 + k] / c[42 + k]:5.1f}")
 print(f"  iterations per intersection: {c[16] / max(c[0], 1):.4f}")
