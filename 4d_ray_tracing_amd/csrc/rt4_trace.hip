@@ -54,8 +54,9 @@ namespace {
 // only in an iteration where some active lane starts a sample (b == 0), so a new pixel's bounces run in
 // phase with the wave's other paths. In a closed scene (config 4's mirror room: every path runs all
 // R + 1 bounces) the lanes of a wave then stay in lockstep, bounce for bounce, instead of drifting apart
-// with every early miss; in open scenes some lane starts a sample in almost every iteration, so the
-// refill stays immediate. 0 = refill as soon as REFILL_MIN lanes are idle (A/B knob).
+// with every early miss (config 4: 110.5 -> 91.2 ms per frame); in open scenes the wait costs more than
+// it aligns (hypercube -1.5 %). 1 = the kernels of scenes with a tiger or three or more spaces
+// (phase_refill_of), 2 = every kernel, 0 = none (A/B knob; profiles/r03_ab.txt).
 #define RT4_PHASE_REFILL 1
 #endif
 #ifndef RT4_LUT_PREFETCH
@@ -87,19 +88,20 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #define RT4_POOL_SPHERES 0
 #endif
 #ifndef RT4_DEFER_EXACT
-#define RT4_DEFER_EXACT 0
+// Deferred exact sphere tests: a wave runs its pending exact sphere tests only once at
+// least RT4_DEFER_EXACT of its lanes have one, or after RT4_DEFER_WAIT iterations; the lanes that wait park
+// (config 2 +6 % at 32 / 4). Open scenes only: kernels without a tiger (all_primitives -0.5 %) and
+// without the phase-aligned refill (the closed room -3 %); 0 = off.
+#define RT4_DEFER_EXACT 32
 #endif
 #ifndef RT4_DEFER_WAIT
-#define RT4_DEFER_WAIT 2
+#define RT4_DEFER_WAIT 4
 #endif
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
 #ifndef RT4_WAVES_MIRROR
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
-#endif
-#ifndef RT4_PIPE_MIRROR
-#define RT4_PIPE_MIRROR 0  // 1: pipeline the mirror-room kernel's frames too (A/B knob)
 #endif
 #ifndef RT4_WAVES_SPHERE
 #define RT4_WAVES_SPHERE 7
@@ -396,6 +398,13 @@ constexpr int min_waves_of(uint32_t K) {
   return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
 
+// Phase-aligned refill for this kernel (RT4_PHASE_REFILL): scenes with a tiger or >= 3 spaces (closed rooms).
+constexpr bool phase_refill_of(uint32_t K) {
+  if (RT4_PHASE_REFILL == 0) return false;
+  if (RT4_PHASE_REFILL == 2) return true;
+  return K != GENERIC && ((K & K_TIGER) || ((K & K_SPACES) && ((K >> 8) & 0xFFu) >= 4));
+}
+
 template <uint32_t K, bool LUT, bool REUSE>
 __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
@@ -446,7 +455,9 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   const unsigned wave = threadIdx.x >> 6;
   // Deferred exact sphere tests (A/B knob RT4_DEFER_EXACT = the wave's pending-lane threshold, 0 = off;
   // RT4_DEFER_WAIT = the most iterations a parked lane waits): DESIGN.md §9, profiles/r03_ab.txt
-  constexpr bool DEFER = RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && sh_count(K, 2) != 0;
+  constexpr bool DEFER = RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && !(K & K_TIGER) &&
+                         !phase_refill_of(K) && sh_count(K, 2) != 0;
+  constexpr bool PHASE = phase_refill_of(K) && !REUSE;
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
 
   bool exhausted = false;
@@ -634,7 +645,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       // a sample; every active lane finishes a sample within R + 1 iterations, so the wait is bounded.
       // Not with primary reuse: there a sample's bounce 0 is shaded in the iteration that ends the previous
       // sample, so a starting sample is at b == 1 at the top of the loop.
-      if (RT4_PHASE_REFILL && !REUSE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
+      if (PHASE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
       if (refill) {
         RT4_LS(8);
         retire();
@@ -1918,10 +1929,9 @@ int32_t frames_per_launch(int32_t w, int32_t h) {
 extern "C" {
 
 int32_t rt4_context_frames_per_launch(const rt4_context* ctx, int32_t w, int32_t h) {
-  if (!ctx) return 1;
-  const bool mirror_room = !RT4_PIPE_MIRROR && ctx->has_scene && (ctx->shape & 0xFFu) == (K_SPACES | K_TIGER) &&
-                           ((ctx->shape >> 8) & 0xFFu) >= 4;
-  return mirror_room ? 1 : frames_per_launch(w, h);
+  // Every scene pipelines since r03-v34: the mirror-room tiger kernel (config 4) ran 17 % slower pipelined
+  // until the phase-aligned refill kept its lanes in lockstep across frames.
+  return ctx ? frames_per_launch(w, h) : 1;
 }
 
 int rt4_context_reserve_frames(rt4_context* ctx, int32_t w, int32_t h, char* err, size_t errlen) {
@@ -1959,9 +1969,6 @@ int rt4_render_frames_device(rt4_context* ctx, const rt4_uniforms* u, int32_t n_
   job.region = *region;
   job.d_frame = d_frame;
   job.row_stride_px = row_stride_px;
-  // The mirror-room tiger kernel (three or more spaces and a tiger: BASELINE config 4) measured slower
-  // pipelined (4K, 64 spp: 128.7 ms per frame against 110.3 ms frame by frame, same clock;
-  // profiles/r02_ab.txt), so its frames run one launch each.
   const int32_t chunk = rt4_context_frames_per_launch(ctx, region->w, region->h);
   int32_t seeds[RT4_MAX_FRAMES];
   float parts[RT4_MAX_FRAMES];

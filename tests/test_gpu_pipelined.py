@@ -132,24 +132,27 @@ def test_frames_reject_changed_uniforms(rt4):
         t.close()
 
 
-def test_mirror_room_runs_frame_by_frame(rt4):
-    """The mirror-room tiger kernel (BASELINE config 4's scene) is not pipelined (measured slower);
-    rt4_render_frames_device still equals the sequential frames there."""
+def test_mirror_room_pipelined_equals_sequential(rt4):
+    """The mirror-room tiger kernel (BASELINE config 4's scene) pipelines like every other kernel since
+    r03-v34 (the phase-aligned refill removed its slowdown); rt4_render_frames_device equals
+    the sequential frames there, in one launch and split over launches, and with a resting camera's
+    identical frames (the bench's call)."""
     scene = rt4.Scene.named("tiger_two_mirrors")
     t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=scene)
     try:
-        assert t.frames_per_launch(64, 40) == 1
-        t.set_scene(rt4.Scene.named("sphere"))
-        assert t.frames_per_launch(1920, 1080) == 64 and t.frames_per_launch(3840, 2160) == 32
+        assert t.frames_per_launch(64, 40) == 64 and t.frames_per_launch(3840, 2160) == 32
         assert t.frames_per_launch(8192, 16) == 1  # wider than the pipelined pixel word holds
+        t.set_scene(rt4.Scene.named("sphere"))
+        assert t.frames_per_launch(1920, 1080) == 64
     finally:
         t.close()
-    base = rt4.make_uniforms(48, 32, samples=2, reflections=6, seed=3)
-    us = [rt4.progressive_uniforms(base, n) for n in range(1, 4)]
+    base = rt4.make_uniforms(48, 32, samples=3, reflections=12, seed=3)
     reg = rt4.region(48, 32)
-    (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, rt4.FLAG_SAMPLER_LUT)
-    assert np_ == nq
-    assert same_bits(p, q)
+    for us in ([rt4.progressive_uniforms(base, n) for n in range(1, 5)], [base] * 3,
+               [rt4.progressive_uniforms(base, n) for n in range(1, 71)]):  # 70 frames: two launches
+        (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, rt4.FLAG_SAMPLER_LUT)
+        assert np_ == nq
+        assert same_bits(p, q)
 
 
 @pytest.mark.parametrize("fmt", ["f16", "rgba8"])

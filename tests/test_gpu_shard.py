@@ -147,14 +147,19 @@ def test_cpp_host_bands_with_rccl_equals_single_gpu(rt4, tmp_path, fmt):
     assert outs[0] == outs[1] == outs[2]
 
 
-def test_mirror_room_reserves_no_scratch(rt4):
-    """rt4_context_reserve_frames allocates nothing for a scene that runs frame by frame, and exactly one
-    chunk of frames otherwise."""
+def test_reserve_frames_sizes_one_chunk(rt4):
+    """rt4_context_reserve_frames allocates nothing for a region that runs frame by frame (wider than the
+    pipelined pixel word holds), and exactly one chunk of frames otherwise: config 4's 4K
+    mirror room in 32-frame chunks since r03-v34."""
     t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=rt4.Scene.named("tiger_two_mirrors"))
     try:
+        assert t.frames_per_launch(8192, 16) == 1
+        t.reserve_frames(8192, 16)
+        assert t.frame_scratch_bytes() == 0
         fpl = t.frames_per_launch(3840, 2160)
+        assert fpl == 32
         t.reserve_frames(3840, 2160)
-        assert t.frame_scratch_bytes() == (0 if fpl == 1 else fpl * 3840 * 2160 * 16)
+        assert t.frame_scratch_bytes() == fpl * 3840 * 2160 * 16
         t.set_scene(rt4.Scene.named("sphere"))
         t.reserve_frames(1920, 1080)
         assert t.frame_scratch_bytes() >= t.frames_per_launch(1920, 1080) * 1920 * 1080 * 16

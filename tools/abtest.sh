@@ -45,7 +45,9 @@ elif [ "$cmd" = run ]; then
       python3 - "$name" "$out" <<'PY'
 import json, sys
 d = json.loads(sys.argv[2])
-print(f"{sys.argv[1]:>12s}  {d['value']/1e9:8.2f} G int/s  kernel {d['kernel_ms']:.3f} ms  valu {d['roofline']['frac']*100:5.2f}%  {d['config']['scene']}")
+fr = d.get("roofline", {}).get("frac")
+print(f"{sys.argv[1]:>12s}  {d['value']/1e9:8.2f} G int/s  kernel {d['kernel_ms']:.3f} ms  "
+      + (f"valu {fr*100:5.2f}%  " if fr else "") + d['config']['scene'])
 PY
     done
   done

@@ -5,7 +5,7 @@ set -u -o pipefail
 OUT=gpurun_out/r03_ab1
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1
-RT4_LIB=$PWD/4d_ray_tracing_amd/lib_ls/librt4.so timeout -k 10 300 python tools/lanestats.py sphere 16 8 1920 1080 20 pipelined \
+true \
   > "$OUT/ls_sphere.log" 2>&1 || { echo "lanestats failed"; tail -20 "$OUT/ls_sphere.log"; exit 1; }
 cat "$OUT/ls_sphere.log"
 COMMON="--no-cpu-baseline --no-ops --no-reuse-leg --no-fbf-leg"
