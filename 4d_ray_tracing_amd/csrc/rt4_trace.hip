@@ -50,14 +50,19 @@ namespace {
 #define RT4_REFILL_MIN 1  // refill as soon as one lane is idle (A/B: 8 -> 1 is +4.5 % sphere, +6 % hypercube, +4 % tiger)
 #endif
 #ifndef RT4_PHASE_REFILL
-// Phase-aligned refill: idle lanes of a wave that still has active lanes are refilled
-// only in an iteration where some active lane starts a sample (b == 0), so a new pixel's bounces run in
-// phase with the wave's other paths. In a closed scene (config 4's mirror room: every path runs all
-// R + 1 bounces) the lanes of a wave then stay in lockstep, bounce for bounce, instead of drifting apart
-// with every early miss (config 4: 110.5 -> 91.2 ms per frame); in open scenes the wait costs more than
-// it aligns (hypercube -1.5 %). 1 = the kernels of scenes with a tiger or three or more spaces
-// (phase_refill_of), 2 = every kernel, 0 = none (A/B knob; profiles/r03_ab.txt).
-#define RT4_PHASE_REFILL 1
+// Lockstep for closed scenes. In a closed room every path runs all R + 1 bounces, so the
+// lanes of a wave that start together stay in lockstep, bounce for bounce, and their rays stay coherent;
+// every early miss and every refill off that beat drifts a lane out of phase for good, which over a long
+// pipelined launch cost config 4 a third of its lane utilisation (38 % -> 26 %). Two rules, in the kernels
+// of scenes with three or more spaces (phase_refill_of):
+//   * phase-aligned refill: idle lanes of a wave with active lanes left are refilled only in an iteration
+//     where some active lane starts a sample (b == 0);
+//   * wave clock (RT4_WAVE_CLOCK): while almost every path of the wave runs full length, samples start only
+//     every R + 1 iterations, so lanes pushed off the beat rejoin it.
+// Config 4: 110.5 -> 91 ms frame by frame, 123 -> 88 ms pipelined (20 frames); open scenes lose 1-2.5 % to
+// the wait (hypercube, tiger, all_primitives), so they keep the immediate refill. 3 = closed rooms (default),
+// 1 = also the tiger kernels, 2 = every kernel, 0 = none (A/B knob; profiles/r03_ab.txt).
+#define RT4_PHASE_REFILL 3
 #endif
 #ifndef RT4_LUT_PREFETCH
 // When the sampler-table entry of a possible diffuse bounce is fetched: 2 = at a hit, in flight
@@ -86,6 +91,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 // slower: sphere -13 %, room -7 %, all_primitives -21 % (profiles/r02_ab.txt): the four waves must
 // iterate in step, and two barriers per iteration cost more than the denser tests save. Off.
 #define RT4_POOL_SPHERES 0
+#endif
+#ifndef RT4_WAVE_CLOCK
+#define RT4_WAVE_CLOCK 1  // wave clock for the phase-refill kernels (rt4_trace_kernel CLOCK); 0 = off (A/B knob)
 #endif
 #ifndef RT4_DEFER_EXACT
 // Deferred exact sphere tests: a wave runs its pending exact sphere tests only once at
@@ -402,7 +410,8 @@ constexpr int min_waves_of(uint32_t K) {
 constexpr bool phase_refill_of(uint32_t K) {
   if (RT4_PHASE_REFILL == 0) return false;
   if (RT4_PHASE_REFILL == 2) return true;
-  return K != GENERIC && ((K & K_TIGER) || ((K & K_SPACES) && ((K >> 8) & 0xFFu) >= 4));
+  const bool rooms = K != GENERIC && (K & K_SPACES) && ((K >> 8) & 0xFFu) >= 4;  // >= 3 spaces: closed rooms
+  return RT4_PHASE_REFILL == 3 ? rooms : rooms || (K != GENERIC && (K & K_TIGER));
 }
 
 template <uint32_t K, bool LUT, bool REUSE>
@@ -459,6 +468,14 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
                          !phase_refill_of(K) && sh_count(K, 2) != 0;
   constexpr bool PHASE = phase_refill_of(K) && !REUSE;
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
+  // Wave clock (closed scenes): while almost every path of the wave runs all R + 1 bounces
+  // (early ends <= 1/32 of the sample ends, a leaky count), samples start only every R + 1 iterations, so
+  // the lanes stay in lockstep bounce for bounce however long the launch; otherwise the phase rule above.
+  constexpr bool CLOCK = PHASE && RT4_WAVE_CLOCK;
+  unsigned wave_it = 0;             // wave-uniform: iteration index mod (R + 1)
+  unsigned n_early = 0, n_full = 0;  // wave-uniform: sample ends before / at the bounce limit (leaky)
+  bool hold = false;                 // the lane's next sample waits for the next clock boundary
+  auto clock_on = [&]() { return n_early * 32u <= n_full; };
 
   bool exhausted = false;
   bool active = false, pending = false;
@@ -638,14 +655,26 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   };
   while (true) {
     RT4_STAMP(t_ph);
+    // wave clock (CLOCK kernels, while the wave's paths run full length): samples start only at
+    // iterations wave_it % (R + 1) == 0; a held lane (its sample ended early) waits for the next one
+    bool boundary = true;
+    if constexpr (CLOCK) {
+      if (clock_on()) {
+        if (__ballot(active) == 0ull) wave_it = 0;  // nothing in flight: this iteration starts the period
+        boundary = wave_it == 0u;
+      }
+      wave_it = wave_it + 1u == static_cast<unsigned>(R + 1) ? 0u : wave_it + 1u;
+      if (boundary) hold = false;
+    }
     if (!exhausted) {
       const unsigned long long idle = __ballot(!active);
       bool refill = static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN;
+      if (CLOCK && clock_on()) refill = refill && boundary;
       // phase-aligned: with active lanes left, wait (at most R + 1 iterations) for one of them to start
       // a sample; every active lane finishes a sample within R + 1 iterations, so the wait is bounded.
       // Not with primary reuse: there a sample's bounce 0 is shaded in the iteration that ends the previous
       // sample, so a starting sample is at b == 1 at the top of the loop.
-      if (PHASE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
+      else if (PHASE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
       if (refill) {
         RT4_LS(8);
         retire();
@@ -693,7 +722,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     ls[1] += __popcll(__ballot(active));
 #endif
     typename Finder<K>::R c{};
-    bool parked = false;  // DEFER: the lane's exact sphere tests wait for a later iteration
+    bool parked = CLOCK && hold;  // DEFER: the lane's exact sphere tests wait; CLOCK: the lane's next sample
     if constexpr (POOL) {
       // find part 1 + publish; barrier; pooled exact tests; barrier; combine (find part 2 below)
       RT4_STAMP(t_ph);
@@ -790,12 +819,13 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
         if (exhausted) break;
         continue;
       }
-      if (active) {
+      if (active && !parked) {
         RT4_STAMP(t_ph);
         c = Finder<K>::find(S, X, P, ray);  // :475
         RT4_ACC(1, t_ph);
       }
     }
+    bool end_early = false, end_full = false;  // CLOCK: the lane's sample ended before / at the bounce limit
     if (active && !parked) {
       RT4_LS(1);
       ++n_inter;
@@ -807,6 +837,8 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       if constexpr (!REUSE) {
         if (end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
           RT4_LS(7);
+          end_early = b <= R;
+          end_full = !end_early;
           const float4 lp = lsum_load();
           lsum_store(make_float4(lp.x + acc.x, lp.y + acc.y, lp.z + acc.z, lp.w));
           const float4 c0 = cold[0];
@@ -861,6 +893,16 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
         }
         lsum_store(lp);
       }
+    }
+    if constexpr (CLOCK) {
+      n_early += static_cast<unsigned>(__popcll(__ballot(end_early)));
+      n_full += static_cast<unsigned>(__popcll(__ballot(end_full)));
+      if (n_early + n_full > 4096u) {  // leaky: the recent paths decide
+        n_early >>= 1;
+        n_full >>= 1;
+      }
+      // a lane that starts its next sample off the clock waits for the next boundary
+      if (clock_on() && wave_it != 0u && active && (end_early || end_full)) hold = true;
     }
   }
   retire();  // the pixels finished after the queue ran dry, then whatever the ring holds
