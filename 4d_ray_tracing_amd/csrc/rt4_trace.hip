@@ -466,7 +466,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   // RT4_DEFER_WAIT = the most iterations a parked lane waits): DESIGN.md §9, profiles/r03_ab.txt
   constexpr bool DEFER = RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && !(K & K_TIGER) &&
                          !phase_refill_of(K) && sh_count(K, 2) != 0;
-  constexpr bool PHASE = phase_refill_of(K) && !REUSE;
+  constexpr bool PHASE = phase_refill_of(K);
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
   // Wave clock (closed scenes): while almost every path of the wave runs all R + 1 bounces
   // (early ends <= 1/32 of the sample ends, a leaky count), samples start only every R + 1 iterations, so
@@ -475,6 +475,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   unsigned wave_it = 0;             // wave-uniform: iteration index mod (R + 1)
   unsigned n_early = 0, n_full = 0;  // wave-uniform: sample ends before / at the bounce limit (leaky)
   bool hold = false;                 // the lane's next sample waits for the next clock boundary
+  bool use_cached = false;           // REUSE: the lane's next find is its pixel's cached primary candidate
   auto clock_on = [&]() { return n_early * 32u <= n_full; };
 
   bool exhausted = false;
@@ -674,7 +675,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       // a sample; every active lane finishes a sample within R + 1 iterations, so the wait is bounded.
       // Not with primary reuse: there a sample's bounce 0 is shaded in the iteration that ends the previous
       // sample, so a starting sample is at b == 1 at the top of the loop.
-      else if (PHASE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
+      else if (PHASE && !REUSE && refill && ~idle != 0ull) refill = __ballot(active && b == 0) != 0ull;
       if (refill) {
         RT4_LS(8);
         retire();
@@ -723,6 +724,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
 #endif
     typename Finder<K>::R c{};
     bool parked = CLOCK && hold;  // DEFER: the lane's exact sphere tests wait; CLOCK: the lane's next sample
+    bool cached = false;          // CLOCK && REUSE: this iteration's candidate came from the primary cache
     if constexpr (POOL) {
       // find part 1 + publish; barrier; pooled exact tests; barrier; combine (find part 2 below)
       RT4_STAMP(t_ph);
@@ -821,7 +823,17 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       }
       if (active && !parked) {
         RT4_STAMP(t_ph);
-        c = Finder<K>::find(S, X, P, ray);  // :475
+        if constexpr (CLOCK && REUSE) {
+          // with the wave clock a sample's bounce 0 is shaded from the cache at the clock boundary, in its
+          // own iteration (the other lanes do the same in lockstep), instead of in the iteration that ended
+          // the previous sample
+          cached = use_cached;
+          if (cached) c = unpack_cand(cold[512]);
+          else c = Finder<K>::find(S, X, P, ray);  // :475
+          use_cached = false;
+        } else {
+          c = Finder<K>::find(S, X, P, ray);  // :475
+        }
         RT4_ACC(1, t_ph);
       }
     }
@@ -829,7 +841,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     if (active && !parked) {
       RT4_LS(1);
       ++n_inter;
-      ++n_eval;
+      if (!cached) ++n_eval;
       if constexpr (REUSE) {
         if (s == 0 && b == 0) cold[512] = pack_cand(c);  // the pixel's primary candidate
       }
@@ -855,6 +867,10 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       }
       while (REUSE && end) {  // path finished (:478 or :494): accumulate, next sample restarts at the focus
         RT4_LS(7);
+        if (!end_early && !end_full) {
+          end_early = b <= R;
+          end_full = !end_early;
+        }
         const float4 lp0 = lsum_load();
         float4 lp = make_float4(lp0.x + acc.x, lp0.y + acc.y, lp0.z + acc.z, lp0.w);
         const float4 c0 = cold[0];
@@ -873,8 +889,8 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
             // (shader.frag:519-521), so its bounce 0 is the cached candidate, shaded in this same
             // iteration with the sample's own random numbers; no find_intersection is evaluated.
             const Cand pc = unpack_cand(cold[512]);
-            ++n_inter;
             if (!pc.hit) {
+              ++n_inter;
               // a primary miss: every remaining sample is that same sky ray, acc = fma(T, sky, acc)
               // with T = 1, acc = 0 (:477-479), added to the sum sample by sample
               const V3 fl = final_light(S, X, ray.drct);
@@ -886,7 +902,10 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
               }
               active = false;
               pending = true;
+            } else if (CLOCK && clock_on()) {
+              use_cached = true;  // shaded (and counted) at the next clock boundary
             } else {
+              ++n_inter;
               end = shade(pc);  // one bounce; the path goes on next iteration unless bounces ran out
             }
           }
