@@ -555,6 +555,15 @@ template <uint32_t SH>
 __device__ __forceinline__ Cand exact_pending(const SceneAux* __restrict__ X, const PrimEntry* P, const Ray& ray,
                                               const SphereGeo& geo, uint32_t pend, Cand inter) {
   while (pend) {
+#ifdef RT4_LANESTATS  // diagnostic: trips and their active lanes (counter[40], [41]), as in find_cand
+    {
+      const unsigned long long ex = __builtin_amdgcn_read_exec();
+      if (rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+        atomicAdd(rt4_ls_counter + 40, 1ull);
+        atomicAdd(rt4_ls_counter + 41, static_cast<unsigned long long>(__popcll(ex)));
+      }
+    }
+#endif
     const int i = __builtin_ctz(pend);
     pend &= pend - 1u;
     if constexpr (geo_spheres<SH>() > 0)

@@ -838,6 +838,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       }
     }
     bool end_early = false, end_full = false;  // CLOCK: the lane's sample ended before / at the bounce limit
+    if (active && parked) RT4_LS(9);  // lanes waiting (deferred exact tests, or held for the wave clock)
     if (active && !parked) {
       RT4_LS(1);
       ++n_inter;

@@ -40,7 +40,7 @@ ev1.record()
 torch.cuda.synchronize()
 c = cnt.cpu().tolist()
 names = ["loop iteration (active lanes)", "find (active)", "-", "miss", "hit", "reflect", "diffuse", "end of sample",
-         "refill", "-"]
+         "refill", "parked / held"]
 print(f"{scene} {W}x{H} spp={spp} bounces={bounces} frames={frames} {mode} frames/launch="
       f"{t.frames_per_launch(W, H) if mode == 'pipelined' else 1}: intersections={c[0]}, "
       f"{ev0.elapsed_time(ev1) / frames:.3f} ms/frame (lanestats build)")
