@@ -354,6 +354,15 @@ __device__ __forceinline__ Cand hypercube_cand(const rt4_scene_desc* __restrict_
     }
     Cand res = no_cand();
     while (cand) {
+#ifdef RT4_LANESTATS  // diagnostic: pending-cell trips and their active lanes (counter[58], [59])
+      {
+        const unsigned long long ex = __builtin_amdgcn_read_exec();
+        if (rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+          atomicAdd(rt4_ls_counter + 58, 1ull);
+          atomicAdd(rt4_ls_counter + 59, static_cast<unsigned long long>(__popcll(ex)));
+        }
+      }
+#endif
       const int k = __builtin_ctz(cand);
       cand &= cand - 1u;
       float dist;

@@ -802,6 +802,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
         if (exhausted) break;
         continue;
       }
+      RT4_STAMP(t_ph);
       uint32_t pend = 0;
       SphereGeo geo;
       Cand inter = no_cand();
@@ -816,6 +817,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
         defer_age = 0;
       }
       if (active && !parked) c = find_rest<K>(S, X, P, ray, exact_pending<K>(X, P, ray, geo, pend, inter));
+      RT4_ACC(1, t_ph);
     } else {
       if (!__any(active)) {
         if (exhausted) break;

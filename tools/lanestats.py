@@ -52,6 +52,9 @@ for p, n in enumerate(names):
 if c[40]:
     print(f"  {'exact sphere test (pending)':>30s}: {c[40]:12d} wave execs ({c[40] / max(c[16], 1):5.3f} per iteration), "
           f"{c[41] / c[40]:5.1f} lanes avg")
+if c[58]:
+    print(f"  {'hypercube cell test (pending)':>30s}: {c[58]:12d} wave execs ({c[58] / max(c[16], 1):5.3f} per iteration), "
+          f"{c[59] / c[58]:5.1f} lanes avg")
 if any(c[42:49]):
     tot = sum(c[42:49])
     print("  finds with pending spheres, by lanes pending (wave events share, lanes avg):")
