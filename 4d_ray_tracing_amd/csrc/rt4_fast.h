@@ -536,7 +536,7 @@ __device__ __forceinline__ Cand sphere_exact(const SceneAux* __restrict__ X, con
   return sphere_cand(ld4(e.p), e.r, dc, ray, true, id);
 }
 
-template <uint32_t SH>
+template <uint32_t SH, bool WITH_TIGER = true>
 __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
                                           const PrimEntry* P, const Ray& ray, Cand inter) {
   constexpr uint32_t K = SH & 0xFFu;
@@ -553,8 +553,19 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
   if (K & K_UNION)
     if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
   if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && !(K & K_TIGER)>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
-  if (K & K_TIGER)
-    if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
+  if ((K & K_TIGER) && WITH_TIGER)
+    if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) {
+#ifdef RT4_LANESTATS  // diagnostic: tiger tests and their active lanes (counter[60], [61])
+      {
+        const unsigned long long ex = __builtin_amdgcn_read_exec();
+        if (rt4_ls_counter && (threadIdx.x & 63u) == static_cast<unsigned>(__builtin_ctzll(ex))) {
+          atomicAdd(rt4_ls_counter + 60, 1ull);
+          atomicAdd(rt4_ls_counter + 61, static_cast<unsigned long long>(__popcll(ex)));
+        }
+      }
+#endif
+      inter = closest(tiger_cand(S, X, 0, B.tiger, ray), inter);
+    }
   return inter;
 }
 
@@ -583,7 +594,7 @@ __device__ __forceinline__ Cand exact_pending(const SceneAux* __restrict__ X, co
   return inter;
 }
 
-template <uint32_t SH>
+template <uint32_t SH, bool WITH_TIGER = true>
 __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X,
                                           const PrimEntry* P, const Ray& ray) {
   constexpr uint32_t K = SH & 0xFFu;
@@ -626,7 +637,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
         inter = closest(sphere_exact<SH>(X, P, ray, i), inter);
     }
   }
-  return find_rest<SH>(S, X, P, ray, inter);
+  return find_rest<SH, WITH_TIGER>(S, X, P, ray, inter);
 #else
   constexpr uint32_t NSP = sh_count(SH, 1), NSH = sh_count(SH, 2);
   const PrimBases B = prim_bases<SH>(X);
@@ -638,7 +649,7 @@ __device__ __forceinline__ Cand find_cand(const rt4_scene_desc* __restrict__ S, 
       inter = closest(sphere_cand(ld4(sp.center), sp.r, X->sphere_r[i], ray, true, B.sphere + static_cast<uint32_t>(i)),
                       inter);
     });
-  return find_rest<SH>(S, X, P, ray, inter);
+  return find_rest<SH, WITH_TIGER>(S, X, P, ray, inter);
 #endif
 }
 

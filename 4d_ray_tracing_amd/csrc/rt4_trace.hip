@@ -98,6 +98,12 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_WAVE_CLOCK
 #define RT4_WAVE_CLOCK 1  // wave clock for the phase-refill kernels (rt4_trace_kernel CLOCK); 0 = off (A/B knob)
 #endif
+#ifndef RT4_DEFER_TIGER
+#define RT4_DEFER_TIGER 32  // deferred tiger tests: the wave's lane threshold (rt4_trace_kernel TDEFER); 0 = off
+#endif
+#ifndef RT4_DEFER_TIGER_WAIT
+#define RT4_DEFER_TIGER_WAIT 4
+#endif
 #ifndef RT4_DEFER_EXACT
 // Deferred exact sphere tests: a wave runs its pending exact sphere tests only once at
 // least RT4_DEFER_EXACT of its lanes have one, or after RT4_DEFER_WAIT iterations; the lanes that wait park
@@ -479,6 +485,13 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   unsigned n_early = 0, n_full = 0;  // wave-uniform: sample ends before / at the bounce limit (leaky)
   bool hold = false;                 // the lane's next sample waits for the next clock boundary
   bool use_cached = false;           // REUSE: the lane's next find is its pixel's cached primary candidate
+  // Deferred tiger tests (open scenes with a tiger): a lane whose ray reaches the tiger's
+  // bounding ball keeps its candidate of every other group (cold[512], pack_cand) and waits until at least
+  // RT4_DEFER_TIGER lanes of the wave need the tiger test, or RT4_DEFER_TIGER_WAIT iterations; then the
+  // tiger runs last, as in find_rest (closest(tiger, the rest): the same bits).
+  constexpr bool TDEFER = RT4_DEFER_TIGER > 0 && !REUSE && K != GENERIC && (K & K_TIGER) && !PHASE;
+  bool tparked = false;              // TDEFER: the lane waits for the tiger test with its candidate in cold[512]
+  int tdefer_age = 0;                // TDEFER, wave-uniform
   auto clock_on = [&]() { return n_early * 32u <= n_full; };
 
   bool exhausted = false;
@@ -490,7 +503,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   // [0] the pixel's primary direction d0, [256] {light sum, pack_pixel()}. Touched once per sample,
   // so the VGPRs go to occupancy instead (6 -> 7 waves/SIMD on the sphere scene).
   // [512]: the pixel's primary candidate (RT4_FLAG_PRIMARY_REUSE; pack_cand)
-  __shared__ float4 lds_cold[(REUSE ? 3 : 2) * 256];
+  __shared__ float4 lds_cold[(REUSE || TDEFER ? 3 : 2) * 256];
   float4* const cold = lds_cold + threadIdx.x;
   // RT4_LSUM_REG (specialised kernels without a tiger or a hypercube): {light sum, pack_pixel()} stays
   // in 4 VGPRs instead of cold[256], so the end of a sample is three register adds instead of an LDS
@@ -815,6 +828,41 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
           nb += static_cast<unsigned>(__popcll(qm));
         }
         c = find_rest<K>(S, X, P, ray, inter);
+      }
+      RT4_ACC(1, t_ph);
+    } else if constexpr (TDEFER) {
+      if (!__any(active)) {
+        if (exhausted) break;
+        continue;
+      }
+      RT4_STAMP(t_ph);
+      Cand pre = no_cand();
+      bool need = false;
+      if (active) {
+        if (tparked) {
+          pre = unpack_cand(cold[512]);
+          need = true;
+        } else {
+          pre = find_cand<K, false>(S, X, P, ray);  // every group but the tiger, in order
+          need = !(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray));
+        }
+      }
+      const unsigned long long tm = __ballot(need);
+      const bool run = tm != 0ull && (static_cast<unsigned>(__popcll(tm)) >= static_cast<unsigned>(RT4_DEFER_TIGER) ||
+                                      tdefer_age >= RT4_DEFER_TIGER_WAIT || tm == __ballot(active));
+      if (tm != 0ull && !run) {
+        ++tdefer_age;
+        if (need) {
+          if (!tparked) cold[512] = pack_cand(pre);
+          tparked = true;
+          parked = true;
+        }
+      } else {
+        tdefer_age = 0;
+      }
+      if (active && !parked) {
+        c = need ? closest(tiger_cand(S, X, 0, prim_bases<K>(X).tiger, ray), pre) : pre;  // find_rest's last group
+        tparked = false;
       }
       RT4_ACC(1, t_ph);
     } else if constexpr (DEFER) {

@@ -55,6 +55,9 @@ if c[40]:
 if c[58]:
     print(f"  {'hypercube cell test (pending)':>30s}: {c[58]:12d} wave execs ({c[58] / max(c[16], 1):5.3f} per iteration), "
           f"{c[59] / c[58]:5.1f} lanes avg")
+if c[60]:
+    print(f"  {'tiger test':>30s}: {c[60]:12d} wave execs ({c[60] / max(c[16], 1):5.3f} per iteration), "
+          f"{c[61] / c[60]:5.1f} lanes avg")
 if any(c[42:49]):
     tot = sum(c[42:49])
     print("  finds with pending spheres, by lanes pending (wave events share, lanes avg):")
