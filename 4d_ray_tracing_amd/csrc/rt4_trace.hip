@@ -95,6 +95,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_CLAIM_TILES
 #define RT4_CLAIM_TILES 4  // 8x8 tiles per queue atomic in pipelined launches (rt4_trace_kernel CLAIM_TILES)
 #endif
+#ifndef RT4_CLAIM_TILES_DEFER
+#define RT4_CLAIM_TILES_DEFER 1  // the same for the deferred-sphere kernel (A/B knob)
+#endif
 #ifndef RT4_WAVE_CLOCK
 #define RT4_WAVE_CLOCK 1  // wave clock for the phase-refill kernels (rt4_trace_kernel CLOCK); 0 = off (A/B knob)
 #endif
@@ -532,13 +535,15 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   __shared__ float4 lds_out[256];
   const unsigned wbase = threadIdx.x & ~63u;
   unsigned in_next = 64;  // wave-uniform: next inbox entry to hand out (64: empty)
-  // RT4_CLAIM_TILES > 1: one atomic claims that many consecutive tiles; the spare ones are used in turn
-  // (wave-uniform). A spare position past the end of the queue reports it exhausted like a fresh claim.
-  unsigned spare_base = 0, spare_n = 0, last_base = 0;
+  // RT4_CLAIM_TILES > 1: one atomic claims that many consecutive tiles; the spare ones are used in turn.
+  // A spare position past the end of the queue reports it exhausted like a fresh claim.
+  // wave-uniform: the position after the last claimed tile | the claimed tiles not handed out yet (queue
+  // positions are multiples of BATCH, so the count fits in the low bits)
+  unsigned spare = 0;
   // Tiles per queue atomic: fewer round trips to the one contended queue word. Measured
   // (profiles/r03_ab.txt): hypercube +3.7 % at 2, all_primitives +4.6 % and the mirror room +1.4 % at 4,
   // but the sphere kernel with deferred exact tests -5..-7 %: it keeps one.
-  constexpr unsigned CLAIM_TILES = DEFER ? 1u : static_cast<unsigned>(RT4_CLAIM_TILES);
+  constexpr unsigned CLAIM_TILES = static_cast<unsigned>(DEFER ? RT4_CLAIM_TILES_DEFER : RT4_CLAIM_TILES);
   uint32_t in_seed = useed;  // wave-uniform: the seed of the inbox's frame
   unsigned ring_n = 0;    // wave-uniform: outbox entries waiting to be written
   int s = 0, b = 0;
@@ -594,20 +599,18 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   // the queue is exhausted.
   auto claim_batch = [&]() -> bool {
     unsigned base = 0;
-    if (CLAIM_TILES > 1 && spare_n > 0u) {  // the next tile of the last claim: no atomic round trip
-      base = spare_base;
-      spare_base += BATCH;
-      --spare_n;
+    if (CLAIM_TILES > 1 && (spare & (BATCH - 1u)) != 0u) {  // the next tile of the last claim: no atomic
+      base = spare & ~(BATCH - 1u);
+      spare += BATCH - 1u;  // the next position, one tile fewer
     } else {
       // several tiles per claim only in pipelined launches and before their last frame, so the drain at
       // the end of the launch still hands out single tiles
-      const unsigned nt = (CLAIM_TILES > 1 && a.n_frames > 1 && last_base + a.frame_tiles * BATCH < total)
-                              ? CLAIM_TILES : 1u;
+      const unsigned nt =
+          (CLAIM_TILES > 1 && a.n_frames > 1 && (spare & ~(BATCH - 1u)) + a.frame_tiles * BATCH < total) ? CLAIM_TILES
+                                                                                                         : 1u;
       if (lane == 0) base = atomicAdd(queue, BATCH * nt);
       base = __builtin_amdgcn_readfirstlane(base);
-      last_base = base;
-      spare_base = base + BATCH;
-      spare_n = nt - 1u;
+      spare = (base + BATCH) | (nt - 1u);
     }
     if (base >= total) return false;
     // a 64-pixel batch is one tile of one job (of one frame): wave-uniform here (scalar loads)

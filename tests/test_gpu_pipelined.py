@@ -230,3 +230,34 @@ def test_config5_chunk_pipelined_equals_sequential(rt4):
     (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 1, rt4.FLAG_SAMPLER_LUT, reserve=True)
     assert np_ == nq
     assert same_bits(p, q)
+
+
+def test_config4_pipelined_equals_sequential(rt4):
+    """BASELINE config 4's launch shape since r03-v35: the mirror room at 3840x2160, 64 spp, 12 bounces,
+    frames pipelined under the wave clock with four tiles per queue claim (§4.26), against
+    frame-by-frame launches, bit for bit, count included: three identical frames (the bench's call) and
+    three progressive ones."""
+    scene = rt4.Scene.named("tiger_two_mirrors")
+    base = rt4.make_uniforms(3840, 2160, samples=64, reflections=12, seed=12345)
+    reg = rt4.region(3840, 2160)
+    for identical, us in ((True, [base] * 3), (False, [rt4.progressive_uniforms(base, n) for n in range(1, 4)])):
+        (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, rt4.FLAG_SAMPLER_LUT, reserve=True)
+        assert np_ == nq
+        if identical:
+            assert np_ == 3 * 6898035764  # the config-4 frame's count (profiles/r03_v38/bench_c4.log)
+        assert same_bits(p, q)
+
+
+@pytest.mark.parametrize("name", ["tiger", "room", "sphere"])
+def test_lockstep_and_deferral_kernels_1080p(rt4, name):
+    """The scheduling rules of round 3 at a full 1080p frame (16 spp, 8 bounces, 6 progressive frames):
+    deferred tiger tests and four-tile claims (tiger), the wave clock (room), deferred exact sphere tests
+    (sphere); pipelined against frame by frame, bit for bit, and with primary reuse."""
+    scene = rt4.Scene.named(name)
+    base = rt4.make_uniforms(1920, 1080, samples=16, reflections=8, seed=777)
+    us = [rt4.progressive_uniforms(base, n) for n in range(1, 7)]
+    reg = rt4.region(1920, 1080)
+    for flags in (rt4.FLAG_SAMPLER_LUT, rt4.FLAG_SAMPLER_LUT | rt4.FLAG_PRIMARY_REUSE):
+        (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, flags)
+        assert np_ == nq
+        assert same_bits(p, q)
