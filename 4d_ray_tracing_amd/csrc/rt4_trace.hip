@@ -96,7 +96,7 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #define RT4_CLAIM_TILES 4  // 8x8 tiles per queue atomic in pipelined launches (rt4_trace_kernel CLAIM_TILES)
 #endif
 #ifndef RT4_CLAIM_TILES_DEFER
-#define RT4_CLAIM_TILES_DEFER 1  // the same for the deferred-sphere kernel (A/B knob)
+#define RT4_CLAIM_TILES_DEFER 4  // the same for the deferred-sphere kernel (needs its 6-wave register budget)
 #endif
 #ifndef RT4_WAVE_CLOCK
 #define RT4_WAVE_CLOCK 1  // wave clock for the phase-refill kernels (rt4_trace_kernel CLOCK); 0 = off (A/B knob)
@@ -123,8 +123,11 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_WAVES_MIRROR
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
+#ifndef RT4_WAVES_ALLPRIM
+#define RT4_WAVES_ALLPRIM 5  // tiger kernels with other groups (all_primitives: BASELINE config 5)
+#endif
 #ifndef RT4_WAVES_SPHERE
-#define RT4_WAVES_SPHERE 7
+#define RT4_WAVES_SPHERE 6
 #endif
 #ifndef RT4_WAVES_EXACT
 #define RT4_WAVES_EXACT 6  // exact-count kernels without a tiger (sphere, room, hypercube, cylinder4d): 6 waves/SIMD
@@ -409,12 +412,14 @@ constexpr int min_waves_of(uint32_t K) {
   if (K == GENERIC) return RT4_WAVES_PER_SIMD;
   if (!(K & K_TIGER)) {
     if ((K >> 8) == 0) return RT4_WAVES_PER_SIMD;  // runtime counts
-    // the one-space sphere kernel (BASELINE config 2): 7 waves (72 VGPRs, 16 B/lane spill) measured
-    // +1-2.5 % over 6 with pipelined frames; the hypercube kernel -1.3 % at 7 (profiles/r02_ab.txt)
+    // the one-space sphere kernel (BASELINE config 2): 6 waves since r03-v40 (80 VGPRs, 8 B/lane spill):
+    // with the deferred exact tests and four-tile claims it is 12 % faster than at 7 (72 VGPRs, where the
+    // claim state spilled 48 B/lane; profiles/r03_ab.txt); r02 had measured 7 +1-2.5 % over 6 without them.
+    // The hypercube kernel -1.3 % at 7 (profiles/r02_ab.txt)
     if ((K & 0xFFu) == (K_SPACES | K_SPHERES) && ((K >> 8) & 0xFFu) == 2) return RT4_WAVES_SPHERE;
     return RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
   }
-  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return 5;
+  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return RT4_WAVES_ALLPRIM;
   return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
 
