@@ -124,7 +124,7 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
 #ifndef RT4_WAVES_ALLPRIM
-#define RT4_WAVES_ALLPRIM 5  // tiger kernels with other groups (all_primitives: BASELINE config 5)
+#define RT4_WAVES_ALLPRIM 6  // tiger kernels with other groups (all_primitives: BASELINE config 5); r03-v40
 #endif
 #ifndef RT4_WAVES_SPHERE
 #define RT4_WAVES_SPHERE 6
@@ -403,9 +403,10 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
   }
 }
 
-// Waves per SIMD the register allocator must leave room for (measured, profiles/r02_ab.txt): the
-// tiger kernels with other groups (all_primitives, ~107 VGPRs -> 4 waves) run faster at 5 with a small
-// spill (+3.7 % on config 5); the tiger kernel specialised for three or more spaces (the mirror room of
+// Waves per SIMD the register allocator must leave room for (measured, profiles/r02_ab.txt, r03_ab.txt): the
+// tiger kernels with other groups (all_primitives, ~107 VGPRs -> 4 waves) ran faster at 5 with a small
+// spill (+3.7 % on config 5), and since the deferred tiger tests at 6 (+2.9 %, r03-v40); the tiger kernel
+// specialised for three or more spaces (the mirror room of
 // config 4) at 6 (+2.3 %); the one-space tiger kernel and everything else keep the allocator's choice
 // (a 6-wave bound costs the one-space tiger 1.2 %).
 constexpr int min_waves_of(uint32_t K) {
