@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# Historical (round 3, kept for the logged measurements): RT4_PIPE_MIRROR, the knob this script varies, was
+# removed in r03-v35 when the mirror room started pipelining; rebuilding it now gives one binary.
 # A/B: phase-aligned refill (RT4_PHASE_REFILL) x config-4 pipelining (RT4_PIPE_MIRROR), deferred exact sphere
 # tests (RT4_DEFER_EXACT / RT4_DEFER_WAIT), every BASELINE config; lane statistics of config 2 (pending histogram).
 set -u -o pipefail

@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# Historical (round 3, kept for the logged measurements): RT4_PIPE_MIRROR, the knob this script varies, was
+# removed in r03-v35 when the mirror room started pipelining; rebuilding it now gives one binary.
 # Config-4 pipelining probe: per-phase lane statistics of the mirror-room tiger kernel,
 # frame by frame vs pipelined, from the -DRT4_LANESTATS -DRT4_PIPE_MIRROR=1 build (lib_ls).
 set -u -o pipefail

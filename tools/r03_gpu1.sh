@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# Historical (round 3, kept for the logged measurements): RT4_PIPE_MIRROR, the knob this script varies, was
+# removed in r03-v35 when the mirror room started pipelining; rebuilding it now gives one binary.
 # Round-3 first GPU pass: the new parity tests (bench-shape pipelined frames, C++ RCCL bands path,
 # unpermute), the default bench line, and bench-shape profiles of every config, plus config 4 pipelined
 # (the RT4_PIPE_MIRROR=1 variant library) for the pipelined-vs-frame-by-frame counter diff.
