@@ -477,6 +477,55 @@ int rt4_band_plan(int32_t width, int32_t height, int32_t world, int32_t band, in
 }
 
 // ============================================================================ image output
+namespace {
+// One frame row as 8-bit RGB with the RGBA8 rule of rt4_frame_format (float channels clamped to [0, 1],
+// u = (uint8)(v * 255 + 0.5)); shared by the PPM and PNG writers.
+void rgb8_row(const void* frame, int32_t format, int32_t px_bytes, int32_t w, int64_t row_stride_px, int32_t i,
+              unsigned char* row) {
+  auto q8 = [](float v) {
+    return static_cast<unsigned char>(static_cast<uint32_t>(std::fmin(std::fmax(v, 0.0f), 1.0f) * 255.0f + 0.5f));
+  };
+  const unsigned char* base = static_cast<const unsigned char*>(frame) + static_cast<size_t>(i) * row_stride_px * px_bytes;
+  for (int32_t j = 0; j < w; j++) {
+    const unsigned char* px = base + static_cast<size_t>(j) * px_bytes;
+    for (int c = 0; c < 3; c++) {
+      unsigned char v;
+      if (format == RT4_FRAME_RGBA8) {
+        v = px[c];
+      } else if (format == RT4_FRAME_RGBA16F) {
+        uint16_t hb;
+        std::memcpy(&hb, px + 2 * c, 2);
+        v = q8(rt4_half_to_float(hb));
+      } else {
+        float fv;
+        std::memcpy(&fv, px + 4 * c, 4);
+        v = q8(fv);
+      }
+      row[static_cast<size_t>(j) * 3 + c] = v;
+    }
+  }
+}
+
+uint32_t crc32_png(const unsigned char* p, size_t n, uint32_t c = 0xFFFFFFFFu) {  // PNG / zlib CRC-32
+  for (size_t k = 0; k < n; k++) {
+    c ^= p[k];
+    for (int b = 0; b < 8; b++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+  }
+  return c;
+}
+void put_be32(std::vector<unsigned char>& v, uint32_t x) {
+  for (int s = 24; s >= 0; s -= 8) v.push_back(static_cast<unsigned char>(x >> s));
+}
+bool png_chunk(std::FILE* f, const char* type, const std::vector<unsigned char>& data) {
+  std::vector<unsigned char> buf;
+  put_be32(buf, static_cast<uint32_t>(data.size()));
+  buf.insert(buf.end(), type, type + 4);
+  buf.insert(buf.end(), data.begin(), data.end());
+  put_be32(buf, crc32_png(buf.data() + 4, buf.size() - 4) ^ 0xFFFFFFFFu);
+  return std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+}
+}  // namespace
+
 int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
                   char* err, size_t errlen) {
   if (!path || !frame || w <= 0 || h <= 0 || row_stride_px < w)
@@ -487,35 +536,55 @@ int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w
   if (!f) return rt4_set_err(err, errlen, "cannot open %s for writing", path), RT4_ERR_IO;
   std::fprintf(f, "P6\n%d %d\n255\n", w, h);
   std::vector<unsigned char> row(static_cast<size_t>(w) * 3);
-  auto q8 = [](float v) {  // the RGBA8 rule of rt4_frame_format
-    return static_cast<unsigned char>(static_cast<uint32_t>(std::fmin(std::fmax(v, 0.0f), 1.0f) * 255.0f + 0.5f));
-  };
   for (int32_t i = 0; i < h; i++) {
-    const unsigned char* base = static_cast<const unsigned char*>(frame) + static_cast<size_t>(i) * row_stride_px * px_bytes;
-    for (int32_t j = 0; j < w; j++) {
-      const unsigned char* px = base + static_cast<size_t>(j) * px_bytes;
-      for (int c = 0; c < 3; c++) {
-        unsigned char v;
-        if (format == RT4_FRAME_RGBA8) {
-          v = px[c];
-        } else if (format == RT4_FRAME_RGBA16F) {
-          uint16_t hb;
-          std::memcpy(&hb, px + 2 * c, 2);
-          v = q8(rt4_half_to_float(hb));
-        } else {
-          float fv;
-          std::memcpy(&fv, px + 4 * c, 4);
-          v = q8(fv);
-        }
-        row[static_cast<size_t>(j) * 3 + c] = v;
-      }
-    }
+    rgb8_row(frame, format, px_bytes, w, row_stride_px, i, row.data());
     if (std::fwrite(row.data(), 1, row.size(), f) != row.size()) {
       std::fclose(f);
       return rt4_set_err(err, errlen, "write failed: %s", path), RT4_ERR_IO;
     }
   }
   if (std::fclose(f) != 0) return rt4_set_err(err, errlen, "close failed: %s", path), RT4_ERR_IO;
+  return RT4_OK;
+}
+
+int rt4_write_png(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                  char* err, size_t errlen) {
+  if (!path || !frame || w <= 0 || h <= 0 || row_stride_px < w || static_cast<int64_t>(w) * 3 + 1 > 65535)
+    return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
+  const int32_t px_bytes = rt4_frame_format_bytes(format);
+  if (px_bytes == 0) return rt4_set_err(err, errlen, "unknown frame format %d", format), RT4_ERR_ARG;
+  // 8-bit RGB, filter 0 on every row, zlib stream of stored (uncompressed) deflate blocks: one block per row
+  // (a row of w * 3 + 1 bytes fits a stored block's 65535-byte limit), then Adler-32
+  const size_t rb = static_cast<size_t>(w) * 3 + 1;
+  std::vector<unsigned char> z = {0x78, 0x01};
+  uint32_t a1 = 1, a2 = 0;
+  std::vector<unsigned char> row(rb);
+  for (int32_t i = 0; i < h; i++) {
+    row[0] = 0;
+    rgb8_row(frame, format, px_bytes, w, row_stride_px, i, row.data() + 1);
+    z.push_back(i + 1 == h ? 1 : 0);  // BFINAL, BTYPE 00
+    z.push_back(static_cast<unsigned char>(rb & 0xFF));
+    z.push_back(static_cast<unsigned char>(rb >> 8));
+    z.push_back(static_cast<unsigned char>(~rb & 0xFF));
+    z.push_back(static_cast<unsigned char>((~rb >> 8) & 0xFF));
+    z.insert(z.end(), row.begin(), row.end());
+    for (unsigned char c : row) {
+      a1 = (a1 + c) % 65521u;
+      a2 = (a2 + a1) % 65521u;
+    }
+  }
+  put_be32(z, (a2 << 16) | a1);
+  std::vector<unsigned char> ihdr;
+  put_be32(ihdr, static_cast<uint32_t>(w));
+  put_be32(ihdr, static_cast<uint32_t>(h));
+  ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});  // 8 bits, RGB, deflate, filter 0, no interlace
+  std::FILE* f = std::fopen(path, "wb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s for writing", path), RT4_ERR_IO;
+  static const unsigned char sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+  bool ok = std::fwrite(sig, 1, 8, f) == 8 && png_chunk(f, "IHDR", ihdr) && png_chunk(f, "IDAT", z) &&
+            png_chunk(f, "IEND", {});
+  if (std::fclose(f) != 0) ok = false;
+  if (!ok) return rt4_set_err(err, errlen, "write failed: %s", path), RT4_ERR_IO;
   return RT4_OK;
 }
 

@@ -15,6 +15,7 @@
 //                   [-f f32|f16|rgba8] [--seed S] [-o prefix] [-d device] [--keys WASD...] [--move-seconds t]
 //                   [--frame-by-frame]  (one section and a resting camera: rt4_render_frames_device unless given)
 //                   [--gpus N [--band B]]  (one section, resting camera: bands over devices 0..N-1 + RCCL gather)
+//                   [--png]  (PNG images instead of PPM)
 //                   [--resume ckpt] [--checkpoint ckpt]  (one section: continue / save the progressive
 //                   accumulator, rt4_accum_load / rt4_accum_save; the reference has no counterpart)
 #include <hip/hip_runtime.h>
@@ -213,6 +214,7 @@ int main(int argc, char** argv) {
   uint32_t seed = 12345, keys = 0;
   float move_seconds = 0.0f;
   std::string resume_path, checkpoint_path;
+  bool png = false;
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -236,6 +238,7 @@ int main(int argc, char** argv) {
     else if (a == "--band") band = std::atoi(next());
     else if (a == "--resume") resume_path = next();
     else if (a == "--checkpoint") checkpoint_path = next();
+    else if (a == "--png") png = true;
     else die("unknown argument", a.c_str());
   }
   const int32_t format = fmt_name == "f16" ? RT4_FRAME_RGBA16F : fmt_name == "rgba8" ? RT4_FRAME_RGBA8 : RT4_FRAME_RGBA32F;
@@ -308,8 +311,8 @@ int main(int argc, char** argv) {
     double ms = 0.0;
     const std::vector<unsigned char> img =
         render_bands(gpus, band, scene, us, cw[0], ch[0], format, frame_by_frame, &count, &ms);
-    const std::string path = out + "_yxz.ppm";
-    RT4_CHECK(rt4_write_ppm(path.c_str(), img.data(), format, cw[0], ch[0], cw[0], err, sizeof err));
+    const std::string path = out + (png ? "_yxz.png" : "_yxz.ppm");
+    RT4_CHECK((png ? rt4_write_png : rt4_write_ppm)(path.c_str(), img.data(), format, cw[0], ch[0], cw[0], err, sizeof err));
     std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[0], ch[0]);
     std::printf("gpus %d, frames %d, images 1, intersections %llu, %.3f ms/frame, %.3e intersections/s\n", gpus,
                 frames, count, ms / frames, static_cast<double>(count) / (ms * 1e-3));
@@ -382,8 +385,8 @@ int main(int argc, char** argv) {
   for (int q = 0; q < n_img; q++) {
     std::vector<unsigned char> host(static_cast<size_t>(cw[q]) * ch[q] * px);
     HIP_CHECK(hipMemcpy(host.data(), d_frame[q], host.size(), hipMemcpyDeviceToHost));
-    const std::string path = out + "_" + names[q] + ".ppm";
-    RT4_CHECK(rt4_write_ppm(path.c_str(), host.data(), format, cw[q], ch[q], cw[q], err, sizeof err));
+    const std::string path = out + "_" + names[q] + (png ? ".png" : ".ppm");
+    RT4_CHECK((png ? rt4_write_png : rt4_write_ppm)(path.c_str(), host.data(), format, cw[q], ch[q], cw[q], err, sizeof err));
     std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[q], ch[q]);
     if (q == 0 && !checkpoint_path.empty()) {
       // frames_done counts camera-resting frames only: a moving camera restarts the blend (frame_number 1)

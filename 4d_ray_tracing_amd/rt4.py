@@ -186,6 +186,7 @@ def _load(path=None):
         "rt4_camera_move": ([POINTER(CameraStruct), c_uint32, c_float], None),
         "rt4_camera_frame_uniforms": ([POINTER(CameraStruct), POINTER(Uniforms), c_int, c_int32, POINTER(Uniforms)], c_int),
         "rt4_write_ppm": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64] + E, c_int),
+        "rt4_write_png": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64] + E, c_int),
         "rt4_render_device_ex": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int32, c_int64, c_void_p,
                                   c_void_p] + E, c_int),
         "rt4_render_host_ex": ([c_void_p, POINTER(Uniforms), POINTER(Region), c_void_p, c_int32, c_int64,
@@ -236,7 +237,7 @@ EXPORTED = (
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
     "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch "
-    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_accum_save rt4_accum_info rt4_accum_load"
+    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_accum_save rt4_accum_info rt4_accum_load rt4_write_png"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -507,6 +508,19 @@ def accum_load(path: str):
     _check(lib.rt4_accum_load(os.fsencode(path), c_void_p(frame.ctypes.data), info["format"], info["w"], info["h"],
                               info["w"], byref(n), byref(sd), err, len(err)), err)
     return frame, n.value, sd.value
+
+
+def write_png(path: str, frame, fmt: int | None = None) -> None:
+    """8-bit RGB PNG of an (h, w, 4) frame, the same pixels as write_ppm (rt4_write_png)."""
+    import numpy as np
+
+    frame = np.ascontiguousarray(frame)
+    if fmt is None:
+        fmt = {np.dtype("float32"): FRAME_RGBA32F, np.dtype("float16"): FRAME_RGBA16F,
+               np.dtype("uint8"): FRAME_RGBA8}[frame.dtype]
+    h, w = frame.shape[:2]
+    err = _errbuf()
+    _check(lib.rt4_write_png(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, err, len(err)), err)
 
 
 def frame_format_bytes(fmt: int) -> int:

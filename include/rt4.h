@@ -274,6 +274,9 @@ int rt4_camera_frame_uniforms(rt4_camera* cam, const rt4_uniforms* base, int sec
  * channels are clamped to [0, 1] and mapped with the RGBA8 rule u = (uint8)(v * 255 + 0.5). */
 int rt4_write_ppm(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
                   char* err, size_t errlen);
+/* The same pixels as an 8-bit RGB PNG (uncompressed deflate blocks, so no zlib dependency); w <= 21844. */
+int rt4_write_png(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                  char* err, size_t errlen);
 
 /* ---- accumulator checkpoint / resume (no reference counterpart) ----------------
  * The reference keeps the progressive average only in the window's texture: old_frame is blended with

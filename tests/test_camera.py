@@ -161,3 +161,45 @@ def test_write_ppm(rt4, tmp_path, fmt):
     src = frame[..., :3].astype(np.float32)
     want = frame[..., :3] if fmt == 2 else (np.clip(src, 0, 1) * np.float32(255) + np.float32(0.5)).astype(np.uint8)
     assert (px == want).all()
+
+
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_write_png_same_pixels_as_ppm(rt4, tmp_path, fmt):
+    """rt4_write_png: a valid PNG (signature, IHDR, CRCs, zlib stream with Adler-32) whose decoded pixels
+    are byte for byte the PPM's (the same RGBA8 rule), in every frame format; a padded row stride too."""
+    import struct
+    import zlib
+
+    rng = np.random.default_rng(10 + fmt)
+    f32 = rng.uniform(-0.2, 1.2, (6, 9, 4)).astype(np.float32)
+    frame = {0: f32, 1: f32.astype(np.float16), 2: (np.clip(f32, 0, 1) * 255 + 0.5).astype(np.uint8)}[fmt]
+    rt4.write_ppm(str(tmp_path / "a.ppm"), frame)
+    rt4.write_png(str(tmp_path / "a.png"), frame)
+    ppm = open(tmp_path / "a.ppm", "rb").read()[len(b"P6\n9 6\n255\n"):]
+    data = open(tmp_path / "a.png", "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, chunks = 8, {}
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        typ, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + n]
+        crc, = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(typ + body)
+        chunks[typ] = body
+        pos += 12 + n
+    assert struct.unpack(">IIBBBBB", chunks[b"IHDR"]) == (9, 6, 8, 2, 0, 0, 0) and b"IEND" in chunks
+    raw = zlib.decompress(chunks[b"IDAT"])  # checks the Adler-32 too
+    rows = [raw[i * 28:(i + 1) * 28] for i in range(6)]
+    assert all(r[0] == 0 for r in rows)
+    assert b"".join(r[1:] for r in rows) == ppm
+    # a padded buffer through the C ABI: the padding columns are not written
+    import ctypes
+    import os
+
+    pad = np.zeros((6, 12, 4), dtype=frame.dtype)
+    pad[:, :9] = frame
+    err = ctypes.create_string_buffer(256)
+    assert rt4.lib.rt4_write_png(os.fsencode(str(tmp_path / "b.png")), ctypes.c_void_p(pad.ctypes.data), fmt, 9, 6, 12,
+                                 err, len(err)) == 0
+    assert open(tmp_path / "b.png", "rb").read() == data
+    assert rt4.lib.rt4_write_png(os.fsencode(str(tmp_path / "c.png")), ctypes.c_void_p(pad.ctypes.data), fmt, 30000, 1,
+                                 30000, err, len(err)) == -1  # a row over a stored block's 65535 bytes
