@@ -359,3 +359,24 @@ def test_cpp_host_program_resume(rt4, tmp_path):
     r = subprocess.run(common[:-4] + ["--seed", "100", "-n", "1", "-o", str(tmp_path / "c"), "--resume",
                                       str(tmp_path / "a.rt4")], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "another --seed" in r.stderr
+
+
+def test_cpp_host_program_png(rt4, tmp_path):
+    """rt4_render --png writes PNGs whose pixels are the PPM's (rt4_write_png; decoded with zlib here)."""
+    import os
+    import struct
+    import subprocess
+    import zlib
+
+    exe = os.path.join(os.path.dirname(rt4.LIB_PATH), "rt4_render")
+    props = os.path.join(os.path.dirname(rt4.LIB_PATH), "..", "..", "properties.txt")
+    common = [exe, "-p", props, "-s", "room", "-W", "96", "-H", "60", "-n", "2", "-f", "f16"]
+    for extra, pre in (([], "a"), (["--png"], "b")):
+        r = subprocess.run(common + ["-o", str(tmp_path / pre)] + extra, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+    ppm = (tmp_path / "a_yxz.ppm").read_bytes()[len(b"P6\n96 60\n255\n"):]
+    png = (tmp_path / "b_yxz.png").read_bytes()
+    n, = struct.unpack(">I", png[33:37])
+    assert png[37:41] == b"IDAT"
+    raw = zlib.decompress(png[41:41 + n])
+    assert b"".join(raw[i * 289 + 1:(i + 1) * 289] for i in range(60)) == ppm
