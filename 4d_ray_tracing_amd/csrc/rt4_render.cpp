@@ -14,8 +14,10 @@
 // Usage: rt4_render [-p properties.txt] [-s scene(.frag|builtin name)] [-n frames] [-3] [-W width -H height]
 //                   [-f f32|f16|rgba8] [--seed S] [-o prefix] [-d device] [--keys WASD...] [--move-seconds t]
 //                   [--frame-by-frame]  (one section and a resting camera: rt4_render_frames_device unless given)
-//                   [--gpus N [--band B]]  (one section, resting camera: bands over devices 0..N-1 + RCCL gather)
+//                   [--gpus N [--band B] [--rehearse]]  (one section, resting camera: bands over devices 0..N-1 +
+//                   RCCL gather; --rehearse: N ranks on device 0, the gather as device copies, for one-GPU tests)
 //                   [--png]  (PNG images instead of PPM)
+//                   [--raw]  (also the frame's bytes as stored, <prefix>_<section>.raw: bit-exact comparisons)
 //                   [--resume ckpt] [--checkpoint ckpt]  (one section: continue / save the progressive
 //                   accumulator, rt4_accum_load / rt4_accum_save; the reference has no counterpart)
 #include <hip/hip_runtime.h>
@@ -80,22 +82,53 @@ struct BandRun {  // one GPU's share of a --gpus run
   double ms = 0.0;  // this rank's wall time from the start barrier to its gather (and, on rank 0, the un-permute)
 };
 
+// Every rank's verdict on one step, agreed before anything collective runs: each rank posts its own
+// result, waits at the barrier and reads them all (the barrier's mutex orders the posts before the reads).
+// A rank that failed never leaves the others waiting in a collective, and no collective sees a null or
+// partly set-up buffer: when any rank failed, every rank skips the gather and the un-permute.
+class Agreement {
+ public:
+  Agreement(int n, Barrier& bar) : ok_(static_cast<size_t>(n), 1), bar_(bar) {}
+  bool all(int rank, bool ok) {
+    ok_[static_cast<size_t>(rank)] = ok ? 1 : 0;
+    bar_.wait();
+    bool all_ok = true;
+    for (char v : ok_) all_ok = all_ok && v;
+    bar_.wait();  // everyone has read before the next step posts again
+    return all_ok;
+  }
+
+ private:
+  std::vector<char> ok_;
+  Barrier& bar_;
+};
+
 // The frames of one section on `gpus` devices: pixel bands dealt round-robin
 // (rt4_band_plan), each rank's frames pipelined in one rt4_render_frames_device call into a padded
 // shard of rows_max rows, one ncclGather of the shards to rank 0 and rt4_bands_unpermute_device there.
 // The image equals a one-GPU render bit for bit (every pixel is independent: shader.frag:104-108).
-// Returns the frame on the host (rank 0's), or exits on an error.
+//
+// rehearse (--rehearse, a test switch for boxes with one GPU): every rank is a host thread with its own
+// context, stream and buffers on device 0, and each rank copies its shard into its slot of rank 0's
+// gathered buffer with hipMemcpyAsync where the real run calls ncclGather; the band plan, the barrier,
+// the agreements and the un-permute are the real ones. fail_rank >= 0 (the RT4_RENDER_FAIL_RANK test hook)
+// makes that rank's set-up fail after its allocations, to exercise the error path.
+// Returns the frame on the host (rank 0's), or exits with status 1 naming the failed rank(s).
 std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc* scene, const std::vector<rt4_uniforms>& us,
-                                        int32_t w, int32_t h, int32_t format, bool frame_by_frame,
-                                        unsigned long long* count_out, double* ms_out) {
+                                        int32_t w, int32_t h, int32_t format, bool frame_by_frame, bool rehearse,
+                                        int fail_rank, unsigned long long* count_out, double* ms_out) {
   const int32_t px = rt4_frame_format_bytes(format);
-  std::vector<ncclComm_t> comms(static_cast<size_t>(gpus));
-  std::vector<int> devs(static_cast<size_t>(gpus));
-  for (int r = 0; r < gpus; r++) devs[static_cast<size_t>(r)] = r;
-  if (ncclCommInitAll(comms.data(), gpus, devs.data()) != ncclSuccess) die("ncclCommInitAll", "failed");
+  std::vector<ncclComm_t> comms(static_cast<size_t>(gpus), nullptr);
+  if (!rehearse) {
+    std::vector<int> devs(static_cast<size_t>(gpus));
+    for (int r = 0; r < gpus; r++) devs[static_cast<size_t>(r)] = r;
+    if (ncclCommInitAll(comms.data(), gpus, devs.data()) != ncclSuccess) die("ncclCommInitAll", "failed");
+  }
   std::vector<BandRun> runs(static_cast<size_t>(gpus));
   std::vector<unsigned char> image(static_cast<size_t>(w) * h * px);
   Barrier bar(gpus);
+  Agreement agree(gpus, bar);
+  void* root_gathered = nullptr;  // rank 0's gathered buffer (rehearse: the other ranks copy into it)
   auto rank_main = [&](int r) {
     BandRun& run = runs[static_cast<size_t>(r)];
     char err[1024] = {0};
@@ -103,34 +136,38 @@ std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc
     void *shard = nullptr, *gathered = nullptr, *img = nullptr;
     unsigned long long* d_count = nullptr;
     hipStream_t stream = nullptr;
-    rt4_region reg;
+    rt4_region reg{0, 0, 0, 0, 0, 0};
     int32_t rows_max = 0;
-    bool ok = hipSetDevice(r) == hipSuccess && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
-    if (!ok) run.error = "hipSetDevice / hipStreamCreate";
+    const int dev = rehearse ? 0 : r;
+    auto fail = [&](const char* what) {
+      if (run.error.empty()) run.error = what;
+      return false;
+    };
+    bool ok = (hipSetDevice(dev) == hipSuccess && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess) ||
+              fail("hipSetDevice / hipStreamCreate");
     if (ok && (rt4_band_plan(w, h, gpus, band, r, &reg, &rows_max, err, sizeof err) != RT4_OK ||
-               rt4_context_create(r, RT4_FLAG_SAMPLER_LUT, &ctx, err, sizeof err) != RT4_OK ||
-               rt4_context_set_scene(ctx, scene, err, sizeof err) != RT4_OK)) {
-      ok = false;
-      run.error = err;
-    }
+               rt4_context_create(dev, RT4_FLAG_SAMPLER_LUT, &ctx, err, sizeof err) != RT4_OK ||
+               rt4_context_set_scene(ctx, scene, err, sizeof err) != RT4_OK))
+      ok = fail(err);
     const size_t shard_bytes = static_cast<size_t>(rows_max) * w * px;
     if (ok) {
-      ok = hipMalloc(&shard, shard_bytes) == hipSuccess && hipMemset(shard, 0, shard_bytes) == hipSuccess &&
-           hipMalloc(&d_count, sizeof *d_count) == hipSuccess && hipMemset(d_count, 0, sizeof *d_count) == hipSuccess;
+      ok = (hipMalloc(&shard, shard_bytes) == hipSuccess && hipMemset(shard, 0, shard_bytes) == hipSuccess &&
+            hipMalloc(&d_count, sizeof *d_count) == hipSuccess && hipMemset(d_count, 0, sizeof *d_count) == hipSuccess) ||
+           fail("device allocation");
       if (ok && r == 0)
-        ok = hipMalloc(&gathered, shard_bytes * gpus) == hipSuccess && hipMalloc(&img, image.size()) == hipSuccess;
-      if (!ok) run.error = "device allocation";
+        ok = (hipMalloc(&gathered, shard_bytes * gpus) == hipSuccess && hipMalloc(&img, image.size()) == hipSuccess) ||
+             fail("device allocation");
     }
-    const bool pipelined = !frame_by_frame && us.size() >= 2 && reg.h > 0 &&
+    const bool pipelined = ok && !frame_by_frame && us.size() >= 2 && reg.h > 0 &&
                            rt4_context_frames_per_launch(ctx, reg.w, reg.h) > 1;
-    if (ok && pipelined && rt4_context_reserve_frames(ctx, reg.w, reg.h, err, sizeof err) != RT4_OK) {
-      ok = false;
-      run.error = err;
-    }
-    if (ok) ok = hipDeviceSynchronize() == hipSuccess;
-    bar.wait();  // every rank set up: start together
+    if (ok && pipelined && rt4_context_reserve_frames(ctx, reg.w, reg.h, err, sizeof err) != RT4_OK) ok = fail(err);
+    if (ok && r == fail_rank) ok = fail("set-up failure injected (RT4_RENDER_FAIL_RANK)");
+    if (ok) ok = hipDeviceSynchronize() == hipSuccess || fail("hipDeviceSynchronize");
+    if (r == 0) root_gathered = gathered;  // read by the other ranks only after the agreement's barrier
+    // every rank set up (the agreement is also the start barrier): otherwise nobody renders or gathers
+    const bool all_set = agree.all(r, ok);
     const auto t0 = std::chrono::steady_clock::now();
-    if (ok && reg.h > 0) {
+    if (all_set && reg.h > 0) {
       int st = RT4_OK;
       if (pipelined) {
         st = rt4_render_frames_device(ctx, us.data(), static_cast<int32_t>(us.size()), &reg, shard, format, w, d_count,
@@ -139,31 +176,31 @@ std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc
         for (size_t f = 0; f < us.size() && st == RT4_OK; f++)
           st = rt4_render_device_ex(ctx, &us[f], &reg, shard, format, w, d_count, stream, err, sizeof err);
       }
-      if (st != RT4_OK) {
-        ok = false;
-        run.error = err;
+      if (st != RT4_OK) ok = fail(err);
+    }
+    // the renders were enqueued everywhere: only then the collective (a launch error skips it on every rank)
+    const bool all_rendered = all_set && agree.all(r, ok);
+    if (all_rendered) {
+      if (rehearse) {
+        ok = (hipMemcpyAsync(static_cast<char*>(root_gathered) + static_cast<size_t>(r) * shard_bytes, shard, shard_bytes,
+                             hipMemcpyDeviceToDevice, stream) == hipSuccess &&
+              hipStreamSynchronize(stream) == hipSuccess) ||
+             fail("rehearsal gather copy");
+        bar.wait();  // every shard is in rank 0's buffer before the un-permute
+      } else if (ncclGather(shard, gathered, shard_bytes, ncclUint8, 0, comms[static_cast<size_t>(r)], stream) !=
+                 ncclSuccess) {
+        ok = fail("ncclGather failed");
       }
+      if (ok && r == 0 &&
+          rt4_bands_unpermute_device(gathered, img, w, h, gpus, band, rows_max, format, stream, err, sizeof err) != RT4_OK)
+        ok = fail(err);
     }
-    // every rank takes part in the gather, also one with an error (its shard is then zeros), so that no
-    // rank waits forever in the collective; the error is reported after it
-    if (ncclGather(shard, gathered, shard_bytes, ncclUint8, 0, comms[static_cast<size_t>(r)], stream) != ncclSuccess &&
-        ok) {
-      ok = false;
-      run.error = "ncclGather failed";
-    }
-    if (ok && r == 0 &&
-        rt4_bands_unpermute_device(gathered, img, w, h, gpus, band, rows_max, format, stream, err, sizeof err) != RT4_OK) {
-      ok = false;
-      run.error = err;
-    }
-    if (hipStreamSynchronize(stream) != hipSuccess && ok) {
-      ok = false;
-      run.error = "hipStreamSynchronize";
-    }
+    if (stream && hipStreamSynchronize(stream) != hipSuccess) ok = fail("hipStreamSynchronize");
     run.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (ok && hipMemcpy(&run.count, d_count, sizeof run.count, hipMemcpyDeviceToHost) != hipSuccess) run.error = "count";
+    if (!all_rendered && ok) fail("skipped: another rank failed");
+    if (ok && hipMemcpy(&run.count, d_count, sizeof run.count, hipMemcpyDeviceToHost) != hipSuccess) fail("count");
     if (ok && r == 0 && hipMemcpy(image.data(), img, image.size(), hipMemcpyDeviceToHost) != hipSuccess)
-      run.error = "image copy";
+      fail("image copy");
     if (shard) (void)hipFree(shard);
     if (gathered) (void)hipFree(gathered);
     if (img) (void)hipFree(img);
@@ -174,18 +211,28 @@ std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc
   std::vector<std::thread> threads;
   for (int r = 0; r < gpus; r++) threads.emplace_back(rank_main, r);
   for (auto& t : threads) t.join();
-  for (auto& c : comms) (void)ncclCommDestroy(c);
+  for (auto& c : comms)
+    if (c) (void)ncclCommDestroy(c);
   unsigned long long count = 0;
   double ms = 0.0;
+  std::string errors;
   for (int r = 0; r < gpus; r++) {
     const BandRun& run = runs[static_cast<size_t>(r)];
-    if (!run.error.empty()) die(("rank " + std::to_string(r)).c_str(), run.error.c_str());
+    if (!run.error.empty()) errors += (errors.empty() ? "rank " : "; rank ") + std::to_string(r) + ": " + run.error;
     count += run.count;
     ms = std::max(ms, run.ms);  // the job's time: the slowest rank
   }
+  if (!errors.empty()) die("--gpus", errors.c_str());
   *count_out = count;
   *ms_out = ms;
   return image;
+}
+
+void write_raw(const std::string& path, const std::vector<unsigned char>& bytes) {  // --raw
+  std::FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) die("--raw", path.c_str());
+  const bool ok = std::fwrite(bytes.data(), 1, bytes.size(), f) == bytes.size();
+  if (std::fclose(f) != 0 || !ok) die("--raw: write failed", path.c_str());
 }
 
 uint32_t keys_from(const char* s) {  // controls.cpp:98-113 key names
@@ -214,7 +261,7 @@ int main(int argc, char** argv) {
   uint32_t seed = 12345, keys = 0;
   float move_seconds = 0.0f;
   std::string resume_path, checkpoint_path;
-  bool png = false;
+  bool png = false, rehearse = false, raw = false;
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -239,6 +286,8 @@ int main(int argc, char** argv) {
     else if (a == "--resume") resume_path = next();
     else if (a == "--checkpoint") checkpoint_path = next();
     else if (a == "--png") png = true;
+    else if (a == "--raw") raw = true;
+    else if (a == "--rehearse") rehearse = true;
     else die("unknown argument", a.c_str());
   }
   const int32_t format = fmt_name == "f16" ? RT4_FRAME_RGBA16F : fmt_name == "rgba8" ? RT4_FRAME_RGBA8 : RT4_FRAME_RGBA32F;
@@ -297,9 +346,13 @@ int main(int argc, char** argv) {
   if (gpus > 0) {  // pixel bands over GPUs 0..gpus-1, one RCCL gather (one section, resting camera)
     if (three || (keys && move_seconds > 0.0f)) die("--gpus", "needs one section and a resting camera");
     if (frames < 1 || band < 1) die("--gpus", "frames and band must be >= 1");
-    int ndev = 0;
-    HIP_CHECK(hipGetDeviceCount(&ndev));
-    if (gpus > ndev) die("--gpus", ("only " + std::to_string(ndev) + " HIP devices").c_str());
+    if (!rehearse) {  // a rehearsal puts every rank on device 0 and reports a missing device per rank
+      int ndev = 0;
+      HIP_CHECK(hipGetDeviceCount(&ndev));
+      if (gpus > ndev) die("--gpus", ("only " + std::to_string(ndev) + " HIP devices").c_str());
+    }
+    const char* fail_env = std::getenv("RT4_RENDER_FAIL_RANK");  // test hook: this rank's set-up fails
+    const int fail_rank = fail_env ? std::atoi(fail_env) : -1;
     std::vector<rt4_uniforms> us;
     for (int n = 1; n <= frames; n++) {
       rt4_uniforms u;
@@ -310,9 +363,10 @@ int main(int argc, char** argv) {
     unsigned long long count = 0;
     double ms = 0.0;
     const std::vector<unsigned char> img =
-        render_bands(gpus, band, scene, us, cw[0], ch[0], format, frame_by_frame, &count, &ms);
+        render_bands(gpus, band, scene, us, cw[0], ch[0], format, frame_by_frame, rehearse, fail_rank, &count, &ms);
     const std::string path = out + (png ? "_yxz.png" : "_yxz.ppm");
     RT4_CHECK((png ? rt4_write_png : rt4_write_ppm)(path.c_str(), img.data(), format, cw[0], ch[0], cw[0], err, sizeof err));
+    if (raw) write_raw(out + "_yxz.raw", img);
     std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[0], ch[0]);
     std::printf("gpus %d, frames %d, images 1, intersections %llu, %.3f ms/frame, %.3e intersections/s\n", gpus,
                 frames, count, ms / frames, static_cast<double>(count) / (ms * 1e-3));
@@ -387,6 +441,7 @@ int main(int argc, char** argv) {
     HIP_CHECK(hipMemcpy(host.data(), d_frame[q], host.size(), hipMemcpyDeviceToHost));
     const std::string path = out + "_" + names[q] + (png ? ".png" : ".ppm");
     RT4_CHECK((png ? rt4_write_png : rt4_write_ppm)(path.c_str(), host.data(), format, cw[q], ch[q], cw[q], err, sizeof err));
+    if (raw) write_raw(out + "_" + names[q] + ".raw", host);
     std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[q], ch[q]);
     if (q == 0 && !checkpoint_path.empty()) {
       // frames_done counts camera-resting frames only: a moving camera restarts the blend (frame_number 1)

@@ -147,6 +147,74 @@ def test_cpp_host_bands_with_rccl_equals_single_gpu(rt4, tmp_path, fmt):
     assert outs[0] == outs[1] == outs[2]
 
 
+def _props_with(tmp_path, spp, bounces):
+    import os
+    import re
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "properties.txt")).read()
+    src = re.sub(r"ray_tracing\.samples = \d+", f"ray_tracing.samples = {spp}", src)
+    src = re.sub(r"ray_tracing\.reflections_amount = \d+", f"ray_tracing.reflections_amount = {bounces}", src)
+    path = tmp_path / "properties.txt"
+    path.write_text(src)
+    return str(path)
+
+
+def _run_render(rt4, args, env=None):
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(rt4.LIB_PATH), "rt4_render")
+    return subprocess.run([exe] + args, capture_output=True, text=True, timeout=600,
+                          env=dict(os.environ, **(env or {})))
+
+
+@pytest.mark.parametrize("config", [2, 4])
+def test_cpp_host_rehearsed_bands_equal_single_gpu(rt4, tmp_path, config):
+    """rt4_render --gpus N --rehearse at N = 2, 3, 8: N host threads, N contexts and padded shards (all on
+    this box's one device), the real band plan, barrier, success agreements and rt4_bands_unpermute_device,
+    with each shard copied into its slot of rank 0's gathered buffer where the 8-GPU run calls ncclGather.
+    The assembled frame equals the single-GPU render bit for bit (--raw: the stored floats), with the same
+    intersection count, on BASELINE configs 2 (sphere, 1920x1080, 16 spp, 8 bounces) and 4 (tiger + two
+    mirrors, 3840x2160, 64 spp, 12 bounces) at their full shapes, two progressive frames pipelined per rank
+    (VERDICT r03 item 3). Reference: windows.cpp:45 (one draw per texture), shader.frag:104-108."""
+    import os
+
+    mirrors = os.path.join(os.path.dirname(__file__), "..", "scenes", "tiger_two_mirrors.frag")
+    scene, W, H, spp, b = {2: ("sphere", 1920, 1080, 16, 8), 4: (mirrors, 3840, 2160, 64, 12)}[config]
+    props = _props_with(tmp_path, spp, b)
+    outs = {}
+    for gpus in (None, 2, 3, 8):
+        pre = str(tmp_path / f"g{gpus}")
+        extra = ["--gpus", str(gpus), "--rehearse"] if gpus else []
+        r = _run_render(rt4, ["-p", props, "-s", scene, "-n", "2", "-W", str(W), "-H", str(H), "--seed", "12345",
+                              "--raw", "-o", pre] + extra)
+        assert r.returncode == 0, r.stderr + r.stdout
+        line = [ln for ln in r.stdout.splitlines() if "intersections" in ln][0]
+        count = int(line.split("intersections ")[1].split(",")[0])
+        outs[gpus] = (open(pre + "_yxz.raw", "rb").read(), count)
+    assert len(outs[None][0]) == W * H * 16 and outs[None][1] > 0
+    for gpus in (2, 3, 8):
+        assert outs[gpus][1] == outs[None][1], (gpus, outs[gpus][1], outs[None][1])
+        assert outs[gpus][0] == outs[None][0], gpus
+
+
+@pytest.mark.parametrize("gpus,rehearse,fail", [(3, True, 2), (8, True, 0), (1, False, 0)])
+def test_cpp_host_bands_failed_rank_skips_the_collective(rt4, tmp_path, gpus, rehearse, fail):
+    """A rank whose set-up fails (RT4_RENDER_FAIL_RANK, after its allocations) makes every rank skip the
+    render, the gather (the copies, or the real ncclGather on a one-rank communicator) and the un-permute:
+    status 1 naming the rank, no hang, no image (the collective must never run on a rank whose
+    buffers are not set up)."""
+    import os
+
+    pre = str(tmp_path / "f")
+    r = _run_render(rt4, ["-p", _props_with(tmp_path, 2, 2), "-s", "sphere", "-n", "3", "-W", "160", "-H", "90",
+                          "--gpus", str(gpus), "-o", pre] + (["--rehearse"] if rehearse else []),
+                    env={"RT4_RENDER_FAIL_RANK": str(fail)})
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert f"rank {fail}: set-up failure injected" in r.stderr, r.stderr
+    assert not os.path.exists(pre + "_yxz.ppm")
+
+
 def test_reserve_frames_sizes_one_chunk(rt4):
     """rt4_context_reserve_frames allocates nothing for a region that runs frame by frame (wider than the
     pipelined pixel word holds), and exactly one chunk of frames otherwise: config 4's 4K

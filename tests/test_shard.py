@@ -139,3 +139,29 @@ def test_c_abi_band_plan_rejects_bad_arguments(rt4):
             rt4.band_plan(*args)
     with pytest.raises(rt4.RT4Error):
         rt4.band_plan(10, 10, 2, 0, band=0)
+
+
+def _rt4_render(rt4):
+    exe = os.path.join(os.path.dirname(rt4.LIB_PATH), "rt4_render")
+    if not os.path.exists(exe):
+        pytest.skip("lib/rt4_render not built")
+    return exe
+
+
+def test_cpp_host_bands_error_path_exits_cleanly(rt4, tmp_path):
+    """rt4_render --gpus N (csrc/rt4_render.cpp render_bands) when a rank's set-up fails: every rank agrees
+    on the failure before anything collective runs, skips the gather and the un-permute, and the program
+    exits with status 1 naming the failed rank, without hanging and without writing an image.
+    Here (no GPU) every rank fails at hipSetDevice; RT4_RENDER_FAIL_RANK makes the outcome the same on a
+    machine with a GPU (test_gpu_shard.py runs the injected failure on the MI355X)."""
+    import subprocess
+
+    exe = _rt4_render(rt4)
+    props = os.path.join(ROOT, "properties.txt")
+    pre = str(tmp_path / "bands")
+    env = dict(os.environ, RT4_RENDER_FAIL_RANK="1")
+    r = subprocess.run([exe, "-p", props, "-s", "sphere", "-n", "2", "-W", "64", "-H", "40", "--gpus", "3",
+                        "--rehearse", "-o", pre], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert "rank 1" in r.stderr, r.stderr
+    assert not os.path.exists(pre + "_yxz.ppm")
