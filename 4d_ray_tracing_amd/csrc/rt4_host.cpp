@@ -20,6 +20,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <unistd.h>  // fsync (rt4_accum_save_key)
+
 #include "../../include/rt4.h"
 #include "rt4_internal.h"
 
@@ -595,24 +597,42 @@ struct AccHeader {  // the file's first 40 bytes (rt4.h), little-endian like eve
   char magic[8];
   int32_t version, w, h, format;
   int64_t frames_done;
-  uint32_t seed, reserved;
+  uint32_t seed, key;  // key: rt4_accum_key of the run (version 2; 0 = not recorded, as in version 1 files)
 };
 static_assert(sizeof(AccHeader) == 40, "checkpoint header layout");
 
 int acc_read_header(std::FILE* f, const char* path, AccHeader& hd, char* err, size_t errlen) {
   if (std::fread(&hd, 1, sizeof hd, f) != sizeof hd || std::memcmp(hd.magic, kAccMagic, sizeof kAccMagic) != 0)
     return rt4_set_err(err, errlen, "%s is not an rt4 accumulator checkpoint", path), RT4_ERR_PARSE;
-  if (hd.version != RT4_ACCUM_VERSION)
-    return rt4_set_err(err, errlen, "%s: checkpoint version %d, expected %d", path, hd.version, RT4_ACCUM_VERSION),
+  if (hd.version != 1 && hd.version != RT4_ACCUM_VERSION)
+    return rt4_set_err(err, errlen, "%s: checkpoint version %d, expected 1 or %d", path, hd.version, RT4_ACCUM_VERSION),
            RT4_ERR_PARSE;
+  if (hd.version == 1) hd.key = 0;
   if (hd.w <= 0 || hd.h <= 0 || rt4_frame_format_bytes(hd.format) == 0 || hd.frames_done < 0)
     return rt4_set_err(err, errlen, "%s: bad checkpoint header", path), RT4_ERR_PARSE;
   return RT4_OK;
 }
 }  // namespace
 
-int rt4_accum_save(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
-                   int64_t frames_done, uint32_t seed, char* err, size_t errlen) {
+// FNV-1a over the bytes that decide a progressive run's image besides seed and part: the scene and the
+// uniforms' samples, bounces, indent, tone-map coefficient, resolution, matrix and camera pose
+uint32_t rt4_accum_key(const rt4_scene_desc* scene, const rt4_uniforms* u) {
+  uint32_t hsh = 2166136261u;
+  auto mix = [&](const void* p, size_t n) {
+    for (size_t i = 0; i < n; i++) hsh = (hsh ^ static_cast<const unsigned char*>(p)[i]) * 16777619u;
+  };
+  if (scene) mix(scene, sizeof *scene);
+  if (u) {
+    rt4_uniforms v = *u;
+    v.seed = 0;
+    v.part = 0.0f;
+    mix(&v, sizeof v);
+  }
+  return hsh == 0u ? 1u : hsh;  // 0 means "not recorded"
+}
+
+int rt4_accum_save_key(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                       int64_t frames_done, uint32_t seed, uint32_t key, char* err, size_t errlen) {
   if (!path || !frame || w <= 0 || h <= 0 || row_stride_px < w || frames_done < 0)
     return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
   const int32_t px_bytes = rt4_frame_format_bytes(format);
@@ -625,16 +645,41 @@ int rt4_accum_save(const char* path, const void* frame, int32_t format, int32_t 
   hd.format = format;
   hd.frames_done = frames_done;
   hd.seed = seed;
-  std::FILE* f = std::fopen(path, "wb");
-  if (!f) return rt4_set_err(err, errlen, "cannot open %s for writing", path), RT4_ERR_IO;
+  hd.key = key;
+  // written next to the target, flushed to the disk, then renamed over it: a crash or a full disk
+  // mid-write leaves the previous checkpoint intact
+  const std::string tmp = std::string(path) + ".tmp";
+  std::FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s for writing", tmp.c_str()), RT4_ERR_IO;
   bool ok = std::fwrite(&hd, 1, sizeof hd, f) == sizeof hd;
   const size_t row = static_cast<size_t>(w) * px_bytes;
   for (int32_t i = 0; ok && i < h; i++)
     ok = std::fwrite(static_cast<const unsigned char*>(frame) + static_cast<size_t>(i) * row_stride_px * px_bytes, 1,
                      row, f) == row;
+  ok = ok && std::fflush(f) == 0 && fsync(fileno(f)) == 0;
   if (std::fclose(f) != 0) ok = false;
-  if (!ok) return rt4_set_err(err, errlen, "write failed: %s", path), RT4_ERR_IO;
+  if (ok && std::rename(tmp.c_str(), path) != 0) ok = false;
+  if (!ok) {
+    std::remove(tmp.c_str());
+    return rt4_set_err(err, errlen, "write failed: %s", path), RT4_ERR_IO;
+  }
   return RT4_OK;
+}
+
+int rt4_accum_save(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                   int64_t frames_done, uint32_t seed, char* err, size_t errlen) {
+  return rt4_accum_save_key(path, frame, format, w, h, row_stride_px, frames_done, seed, 0u, err, errlen);
+}
+
+int rt4_accum_key_of(const char* path, uint32_t* key, char* err, size_t errlen) {
+  if (!path || !key) return rt4_set_err(err, errlen, "bad argument"), RT4_ERR_ARG;
+  std::FILE* f = std::fopen(path, "rb");
+  if (!f) return rt4_set_err(err, errlen, "cannot open %s", path), RT4_ERR_IO;
+  AccHeader hd{};
+  const int rc = acc_read_header(f, path, hd, err, errlen);
+  std::fclose(f);
+  if (rc == RT4_OK) *key = hd.key;
+  return rc;
 }
 
 int rt4_accum_info(const char* path, int32_t* w, int32_t* h, int32_t* format, int64_t* frames_done, uint32_t* seed,

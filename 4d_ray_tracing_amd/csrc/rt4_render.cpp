@@ -329,6 +329,15 @@ int main(int argc, char** argv) {
   rt4_camera cam;
   RT4_CHECK(rt4_camera_init(props, &cam, err, sizeof err));
 
+  // the run's key, checked on --resume and recorded by --checkpoint: the first frame's uniforms (seed and
+  // part aside they are every resting frame's)
+  uint32_t run_key = 0;
+  {
+    rt4_camera c0 = cam;
+    rt4_uniforms u0;
+    RT4_CHECK(rt4_camera_frame_uniforms(&c0, &base[0], sections[0], 0, &u0));
+    run_key = rt4_accum_key(scene, &u0);
+  }
   if ((!resume_path.empty() || !checkpoint_path.empty()) && (three || gpus > 0))
     die("--resume/--checkpoint", "need one section on one GPU");
   // frames already blended into the accumulator (a resumed run continues at frame frames_done + 1)
@@ -340,6 +349,12 @@ int main(int argc, char** argv) {
     RT4_CHECK(rt4_accum_load(resume_path.c_str(), resumed.data(), format, cw[0], ch[0], cw[0], &frames_done, &ck_seed, err,
                              sizeof err));
     if (ck_seed != seed) die("--resume", "the checkpoint was made with another --seed");
+    // the checkpoint's run key (scene, samples, bounces, resolution, camera ...): a checkpoint of
+    // another run would be blended in silently
+    uint32_t ck_key = 0;
+    RT4_CHECK(rt4_accum_key_of(resume_path.c_str(), &ck_key, err, sizeof err));
+    if (ck_key != 0u && ck_key != run_key)
+      die("--resume", "the checkpoint was made with another scene, properties or camera");
     cam.frame_number = static_cast<uint32_t>(frames_done + 1);
   }
 
@@ -445,8 +460,8 @@ int main(int argc, char** argv) {
     std::printf("wrote %s (%d x %d)\n", path.c_str(), cw[q], ch[q]);
     if (q == 0 && !checkpoint_path.empty()) {
       // frames_done counts camera-resting frames only: a moving camera restarts the blend (frame_number 1)
-      RT4_CHECK(rt4_accum_save(checkpoint_path.c_str(), host.data(), format, cw[0], ch[0], cw[0],
-                               static_cast<int64_t>(cam.frame_number) - 1, seed, err, sizeof err));
+      RT4_CHECK(rt4_accum_save_key(checkpoint_path.c_str(), host.data(), format, cw[0], ch[0], cw[0],
+                                   static_cast<int64_t>(cam.frame_number) - 1, seed, run_key, err, sizeof err));
       std::printf("checkpoint %s (%lld frames)\n", checkpoint_path.c_str(), static_cast<long long>(cam.frame_number) - 1);
     }
   }

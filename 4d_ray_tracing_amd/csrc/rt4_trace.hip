@@ -482,7 +482,9 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   const unsigned wave = threadIdx.x >> 6;
   // Deferred exact sphere tests (A/B knob RT4_DEFER_EXACT = the wave's pending-lane threshold, 0 = off;
   // RT4_DEFER_WAIT = the most iterations a parked lane waits): DESIGN.md §9, profiles/r03_ab.txt
-  constexpr bool DEFER = RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && !(K & K_TIGER) &&
+  // (not in the native-math build: the deferral runs find_pre's cull, whose exactness bound assumes the
+  // deterministic fused dot that build un-fuses)
+  constexpr bool DEFER = RT4_SPHERE_CULL && RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && !(K & K_TIGER) &&
                          !phase_refill_of(K) && sh_count(K, 2) != 0;
   constexpr bool PHASE = phase_refill_of(K);
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked

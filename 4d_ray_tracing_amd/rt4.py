@@ -209,6 +209,10 @@ def _load(path=None):
                             POINTER(c_uint32)] + E, c_int),
         "rt4_accum_load": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64, POINTER(c_int64), POINTER(c_uint32)]
                            + E, c_int),
+        "rt4_accum_save_key": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64, c_int64, c_uint32, c_uint32] + E,
+                               c_int),
+        "rt4_accum_key": ([c_void_p, c_void_p], c_uint32),
+        "rt4_accum_key_of": ([c_char_p, POINTER(c_uint32)] + E, c_int),
     }
     tolerant = os.environ.get("RT4_AB_TOLERANT") == "1"  # tools/abtest.sh: older builds lack newer exports
     for name, (argtypes, restype) in sig.items():
@@ -237,7 +241,8 @@ EXPORTED = (
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
     "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch "
-    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_accum_save rt4_accum_info rt4_accum_load rt4_write_png"
+    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_accum_save rt4_accum_info rt4_accum_load rt4_write_png "
+    "rt4_accum_save_key rt4_accum_key rt4_accum_key_of"
 ).split()
 
 if ctypes.sizeof(SceneDesc) != lib.rt4_scene_desc_size() or ctypes.sizeof(Uniforms) != lib.rt4_uniforms_size():
@@ -473,9 +478,10 @@ def write_ppm(path: str, frame, fmt: int | None = None) -> None:
     _check(lib.rt4_write_ppm(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, err, len(err)), err)
 
 
-def accum_save(path: str, frame, frames_done: int, seed: int, fmt: int | None = None) -> None:
-    """Checkpoint of a progressive accumulator (rt4_accum_save): the (h, w, 4) host frame and the number of
-    frames already blended into it, with the base seed of its rt4_progressive_uniforms."""
+def accum_save(path: str, frame, frames_done: int, seed: int, fmt: int | None = None, key: int = 0) -> None:
+    """Checkpoint of a progressive accumulator (rt4_accum_save_key): the (h, w, 4) host frame and the number of
+    frames already blended into it, with the base seed of its rt4_progressive_uniforms and the run's key
+    (accum_key; 0 = not recorded). Written to path + ".tmp" and renamed over path."""
     import numpy as np
 
     frame = np.ascontiguousarray(frame)
@@ -484,8 +490,21 @@ def accum_save(path: str, frame, frames_done: int, seed: int, fmt: int | None = 
                np.dtype("uint8"): FRAME_RGBA8}[frame.dtype]
     h, w = frame.shape[:2]
     err = _errbuf()
-    _check(lib.rt4_accum_save(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, frames_done,
-                              seed & 0xFFFFFFFF, err, len(err)), err)
+    _check(lib.rt4_accum_save_key(os.fsencode(path), c_void_p(frame.ctypes.data), fmt, w, h, w, frames_done,
+                                  seed & 0xFFFFFFFF, key & 0xFFFFFFFF, err, len(err)), err)
+
+
+def accum_key(scene, u) -> int:
+    """The run key a checkpoint records (rt4_accum_key): scene + image-deciding uniforms, not seed or part."""
+    return lib.rt4_accum_key(byref(scene.desc if hasattr(scene, "desc") else scene), byref(u))
+
+
+def accum_key_of(path: str) -> int:
+    """The key a checkpoint was saved with (0: not recorded)."""
+    k = c_uint32()
+    err = _errbuf()
+    _check(lib.rt4_accum_key_of(os.fsencode(path), byref(k), err, len(err)), err)
+    return k.value
 
 
 def accum_info(path: str) -> dict:

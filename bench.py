@@ -54,7 +54,10 @@ PEAK_FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
 # the same peak in VALU lane-operations: 256 CUs x 4 SIMDs x 32 lanes per cycle (a wave64 VALU instruction
 # issues over 2 cycles, MI355X_MICROARCH.md) x 2.4 GHz; 157.3 TFLOP/s counts an fma as 2 FLOP
 PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
-METRIC = "ray-bounce intersections/s per GPU at 1080p·16spp·8bounce; %VALU roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+METRIC = "ray-bounce intersections/s per GPU at 1080p·16spp·8bounce; %VALU roofline"  # BASELINE.json, verbatim
+# `value` is the whole job's rate (the bench contract); at N = 1 it is the metric's per-GPU rate, and for N > 1
+# the line also carries value_per_gpu = value / N
 
 CONFIGS = {  # BASELINE.json configs[1..4]
     2: dict(scene="sphere", width=1920, height=1080, spp=16, bounces=8, format="f32", mode="weak", progressive=False),
@@ -201,6 +204,16 @@ def ops_per_unit(rt4, scene, u, width, height, threads):
     n, ops, sampler_ops = oracle_lib.count_ops(scene.desc, u, reg, threads=threads)
     n = max(n, 1)
     return ops / n, (ops - sampler_ops) / n, n
+
+
+def gather_ceiling():
+    """Random 4-B gathers per second from a 32 MiB table with every CU issuing (the sampler table's size and
+    access pattern; tools/mall_probe.hip on an MI355X, profiles/r03_mall/probe.json), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "r03_mall", "probe.json")))
+        return next(r["G_gathers_per_s"] for r in d["results"] if r["table_mib"] == 32) * 1e9
+    except (OSError, ValueError, KeyError, StopIteration):
+        return None
 
 
 def pmc_profile(config, frames_per_dispatch):
@@ -580,6 +593,21 @@ def main():
                     f"{prof.get('avg_ns', 0) * 1e-6:.4f} ms per frame)")
             if prof and der.get("hbm_bytes_per_launch"):
                 line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per frame)"
+                if prof.get("avg_ns"):
+                    # the north star's "achieved HBM GB/s": the profiled traffic over the profiled trace time per
+                    # frame (memory-side bytes: the sampler gathers are served by the Infinity Cache)
+                    gbps = der["hbm_bytes_per_launch"] / prof["avg_ns"]
+                    line["roofline"]["traffic_gbps"] = gbps
+                    line["roofline"]["traffic_frac_of_hbm_peak"] = gbps / HBM_PEAK_GBPS
+            if prof and der.get("fabric_read_requests") and prof.get("avg_ns"):
+                # the sampler gathers against the measured random-gather ceiling of a 32 MiB table
+                # (tools/mall_probe.hip, profiles/r03_mall/probe.json: every CU issuing 4-B random loads)
+                rate = der["fabric_read_requests"] / (prof["avg_ns"] * 1e-9)
+                line["roofline"]["fabric_read_requests_per_s"] = rate
+                ceiling = gather_ceiling()
+                if ceiling:
+                    line["roofline"]["gather_rate_frac"] = rate / ceiling
+                    line["roofline"]["gather_ceiling_per_s"] = ceiling
             if prof and der.get("ea_read_latency_cycles"):
                 line["roofline"]["ea_read_latency_cycles"] = der["ea_read_latency_cycles"]
         if not args.no_cpu_baseline and world == 1:

@@ -284,11 +284,21 @@ int rt4_write_png(const char* path, const void* frame, int32_t format, int32_t w
  * (controls.cpp:132,181,190). A checkpoint is that texture in its rt4_frame_format plus the number of
  * frames already blended and the base seed, so a resumed run (frames frames_done + 1, ... through
  * rt4_progressive_uniforms) continues the same blend bit for bit.
- * File (little-endian): "RT4ACC1\0", int32 version (1), w, h, format, int64 frames_done, uint32 seed,
- * uint32 reserved (0), then h rows of w pixels, rows top first, no padding. */
-#define RT4_ACCUM_VERSION 1
+ * File (little-endian): "RT4ACC1\0", int32 version (2), w, h, format, int64 frames_done, uint32 seed,
+ * uint32 key (rt4_accum_key of the run, 0 = not recorded; version-1 files hold 0 there and still load),
+ * then h rows of w pixels, rows top first, no padding. A save writes <path>.tmp, flushes it to the disk and
+ * renames it over path, so a failed save leaves the previous checkpoint intact. */
+#define RT4_ACCUM_VERSION 2
 int rt4_accum_save(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
                    int64_t frames_done, uint32_t seed, char* err, size_t errlen);
+/* rt4_accum_save with the run's key, so that a resume can refuse a checkpoint of another run. */
+int rt4_accum_save_key(const char* path, const void* frame, int32_t format, int32_t w, int32_t h, int64_t row_stride_px,
+                       int64_t frames_done, uint32_t seed, uint32_t key, char* err, size_t errlen);
+/* The run's key (never 0): a hash of the scene and of the uniforms that decide the progressive image other
+ * than seed and part (samples, bounces, indent, tone-map coefficient, resolution, matrix, camera pose). */
+uint32_t rt4_accum_key(const rt4_scene_desc* scene, const rt4_uniforms* u);
+/* The key a checkpoint was saved with (0: not recorded). */
+int rt4_accum_key_of(const char* path, uint32_t* key, char* err, size_t errlen);
 /* Header only: any output pointer may be null. RT4_ERR_PARSE for a file that is not a checkpoint. */
 int rt4_accum_info(const char* path, int32_t* w, int32_t* h, int32_t* format, int64_t* frames_done, uint32_t* seed,
                    char* err, size_t errlen);

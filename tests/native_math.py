@@ -7,17 +7,31 @@ move when that definition is swapped for plain library built-ins with the shader
   * CPU: oracle/build/librt4_oracle_native.so (glibc acosf/asinf/sinf/cosf) vs the deterministic oracle;
   * GPU: lib_native/librt4.so (ocml, exact shortcuts compiled out) vs the deterministic kernel and vs the
     native oracle (two different native libms, as two GL drivers would differ).
-Reported per BASELINE config 1-3 (SURVEY.md 8(c)'s fallback definition): the fraction of pixels whose
+Reported per BASELINE config (SURVEY.md 8(c)'s fallback definition): the fraction of pixels whose
 RGB channels are all within 1e-4, the mean and max absolute channel error, the bit-identical pixel
-fraction and the intersection counts.
+fraction and the intersection counts. Configs 1-3 at their full frames; configs 4 and 5 (the tiger, the
+union and the cylinders: the transcendental-heavy intersectors, shader.frag:211-217, :251-294, :317-341) on
+four 8-row bands spread over the 3840x2160 frame (32 rows, 1/67.5 of it), one frame each (config 5: one
+16-spp frame in fp32, so that only the built-ins differ).
 """
 import numpy as np
 
-CONFIGS = {  # BASELINE configs 1-3 (SURVEY.md 8(d))
-    1: ("sphere", 256, 256, 1, 2),
-    2: ("sphere", 1920, 1080, 16, 8),
-    3: ("hypercube", 1920, 1080, 16, 8),
+CONFIGS = {  # BASELINE configs (SURVEY.md 8(d)): scene, frame W x H, spp, bounces, rows (y0, band rows, band step, h)
+    1: ("sphere", 256, 256, 1, 2, None),
+    2: ("sphere", 1920, 1080, 16, 8, None),
+    3: ("hypercube", 1920, 1080, 16, 8, None),
+    4: ("tiger_two_mirrors", 3840, 2160, 64, 12, (266, 8, 540, 32)),
+    5: ("all_primitives", 3840, 2160, 16, 8, (266, 8, 540, 32)),
 }
+
+
+def config_region(rt4, config):
+    """The rendered region of a config: the whole frame, or its row bands (rt4_region band layout)."""
+    _, W, H, _, _, rows = CONFIGS[config]
+    if rows is None:
+        return rt4.region(W, H)
+    y0, band_rows, band_step, h = rows
+    return rt4.region(W, h, 0, y0, band_rows, band_step)
 
 
 def divergence(a, b, n_a=None, n_b=None):

@@ -93,3 +93,8 @@ def test_committed_profiles_cover_every_config_of_the_current_kernel(rt4):
         prof = next((p for p in found if p), None)
         assert prof and prof["derived"].get("hbm_bytes_per_launch", 0) > 0, (cfg, version)
         assert prof["counters"].get("SQ_THREAD_CYCLES_VALU", 0) > 0, (cfg, version)
+
+
+def test_gather_ceiling_is_the_committed_probe():
+    """roofline.gather_rate_frac divides by the measured 32 MiB random-gather ceiling (profiles/r03_mall)."""
+    assert abs(bench.gather_ceiling() - 65.69e9) < 1e6

@@ -359,6 +359,31 @@ def test_cpp_host_program_resume(rt4, tmp_path):
     r = subprocess.run(common[:-4] + ["--seed", "100", "-n", "1", "-o", str(tmp_path / "c"), "--resume",
                                       str(tmp_path / "a.rt4")], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "another --seed" in r.stderr
+    # the run key: another scene, another sample count or another resolution is refused
+    assert rt4.accum_key_of(str(tmp_path / "a.rt4")) != 0
+    for change in (["-s", "room"], ["-p", str(_props_samples(tmp_path, 7))]):
+        args = list(common)
+        i = args.index(change[0])
+        args[i + 1] = change[1]
+        r = subprocess.run(args + ["-n", "1", "-o", str(tmp_path / "d"), "--resume", str(tmp_path / "a.rt4")],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode != 0 and "another scene, properties or camera" in r.stderr, (change, r.stderr)
+    # a failed checkpoint write (the .tmp name taken) keeps the checkpoint being resumed from intact
+    before = (tmp_path / "a.rt4").read_bytes()
+    os.mkdir(str(tmp_path / "a.rt4") + ".tmp")
+    r = subprocess.run(common + ["-n", "1", "-o", str(tmp_path / "e"), "--resume", str(tmp_path / "a.rt4"),
+                                 "--checkpoint", str(tmp_path / "a.rt4")], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and (tmp_path / "a.rt4").read_bytes() == before
+
+
+def _props_samples(tmp_path, samples):
+    import os
+    import re
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "properties.txt")).read()
+    path = tmp_path / f"props_{samples}.txt"
+    path.write_text(re.sub(r"ray_tracing\.samples = \d+", f"ray_tracing.samples = {samples}", src))
+    return path
 
 
 def test_cpp_host_program_png(rt4, tmp_path):
