@@ -120,6 +120,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
+#ifndef RT4_OVERLAP_FRAMES
+#define RT4_OVERLAP_FRAMES 1  // single-frame launches overlap the previous frame's drain
+#endif
 #ifndef RT4_WAVES_MIRROR
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
@@ -316,7 +319,7 @@ struct KernelArgs {
   // (frame_part[f]) into the frame buffer afterwards. Pixel words then pack j | i << 13 | f << 26.
   int32_t n_frames;
   unsigned frame_tiles;  // tiles per frame
-  float4* fcolor;        // n_frames x reg.h x reg.w
+  float4* fcolor;        // n_frames x reg.h x reg.w; also set (n_frames 1) for an overlapped single frame
   int32_t frame_seed[RT4_MAX_FRAMES];
   float frame_part[RT4_MAX_FRAMES];
 };
@@ -326,7 +329,7 @@ __device__ __forceinline__ int region_row(const rt4_region& r, int i) {
 }
 
 // A lane's pixel, packed into one dword of its cold state: region-local j (16 bits) | i (14) | job (2);
-// in a pipelined launch (KernelArgs::n_frames > 1) j (13) | i (13) | frame (6).
+// when the pixels go to the frame-colour scratch (KernelArgs::fcolor) j (13) | i (13) | frame (6).
 __device__ __forceinline__ int pack_pixel(int j, int i, int job) { return j | (i << 16) | (job << 30); }
 __device__ __forceinline__ int pack_pixel_f(int j, int i, int f) { return j | (i << 13) | (f << 26); }
 
@@ -575,8 +578,9 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
     if (lane < ring_n) {
       const float4 lp = lds_out[wbase + lane];
       const int pk = __float_as_int(lp.w);
-      if (a.n_frames > 1) {
-        // pipelined frames: the light sum of frame f as is; rt4_fold_frames_kernel tone-maps and blends
+      if (a.fcolor) {
+        // pipelined or overlapped frames: the light sum of frame f as is; rt4_fold_frames_kernel tone-maps and
+        // blends
         const unsigned j = pk & 0x1FFF, i = (pk >> 13) & 0x1FFF, f = (pk >> 26) & 0x3F;  // < 2^28 pixels (4 GiB)
         const rt4_region& rg = a.jobs[0].reg;
         a.fcolor[(f * static_cast<unsigned>(rg.h) + i) * static_cast<unsigned>(rg.w) + j] = lp;
@@ -647,7 +651,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       dd = divs(dd, length(dd));
       d0 = make_float4(dd.x, dd.y, dd.z, dd.w);
       px = uint2{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ in_seed,
-                 static_cast<uint32_t>(a.n_frames > 1 ? pack_pixel_f(jj, ii, static_cast<int>(frame)) : pack_pixel(jj, ii, job))};
+                 static_cast<uint32_t>(a.fcolor ? pack_pixel_f(jj, ii, static_cast<int>(frame)) : pack_pixel(jj, ii, job))};
     }
     lds_in_d0[threadIdx.x] = d0;
     lds_in_px[threadIdx.x] = px;
@@ -1205,9 +1209,15 @@ __global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, cons
 
 // The frames of a pipelined launch blended in order into the frame buffer (rt4_render_frames_device):
 // per pixel the same blend as write_pixel, frame after frame, each rounded to the frame format.
-__global__ void rt4_fold_frames_kernel(const KernelArgs a) {
+// count_src (an overlapped single frame): the trace kernel's count, moved into the caller's counter here, on
+// the caller's stream, and reset for the slot's next frame
+__global__ void rt4_fold_frames_kernel(const KernelArgs a, unsigned long long* count_src, unsigned long long* count_dst) {
   const JobArgs& J = a.jobs[0];
   const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (count_src && p == 0) {
+    if (count_dst) atomicAdd(count_dst, *count_src);
+    *count_src = 0ull;
+  }
   const int64_t npx = static_cast<int64_t>(J.reg.w) * J.reg.h;
   if (p >= npx) return;
   const int i = static_cast<int>(p / J.reg.w), j = static_cast<int>(p - static_cast<int64_t>(i) * J.reg.w);
@@ -1381,11 +1391,21 @@ struct rt4_context {
   hipStream_t last_stream = nullptr;
   bool launched = false;
   unsigned launch_seq = 0;
-  bool queue_dirty = false;  // a launch failed: the next one zeroes its queue word itself
+  bool queue_dirty = false;  // a launch failed: launch dirty_seq zeroes its queue word itself
+  unsigned dirty_seq = 0;
   unsigned long long* d_eval = nullptr;  // evaluated find calls (RT4_FLAG_PRIMARY_REUSE), rt4_context_evaluated
   int n_cu = 0;
   TraceFn occ_fn = nullptr;  // blocks per CU of the last trace kernel launched (occupancy query cache)
   int occ_per_cu = 0;
+  // Overlapped single frames: launch s traces on side[s % 2] into ofcolor[s % 2] while
+  // launch s - 1 drains; its fold runs on the caller's stream. seq_done[s % 2]: recorded when launch s is
+  // complete (launch s + 2 waits for it: queue word, frame-colour and count slot).
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t traced[2] = {nullptr, nullptr};
+  hipEvent_t seq_done[2] = {nullptr, nullptr};
+  void* d_ofcolor[2] = {nullptr, nullptr};
+  size_t ofcolor_bytes = 0;      // bytes of each slot
+  unsigned long long* d_ocount = nullptr;  // 2 counters, one per slot
 };
 
 #define HIP_TRY(expr)                                                                            \
@@ -1775,6 +1795,13 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (e == hipSuccess) e = hipMemset(c->d_queue, 0, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream's first launch
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  for (int k = 0; k < 2 && e == hipSuccess; k++) {
+    e = hipEventCreateWithFlags(&c->seq_done[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->traced[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(c->seq_done[k], nullptr);  // "launch -2 and -1" are complete
+  }
+  if (e == hipSuccess) e = hipMalloc(&c->d_ocount, 2 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->d_ocount, 0, 2 * sizeof(unsigned long long));
   if (e == hipSuccess) {  // tile order for frames up to 2^18 tiles (16.7 M pixels); larger ones grow it once
     e = hipMalloc(&c->d_order, ((size_t(1) << 18) + 2) * sizeof(unsigned));
     if (e == hipSuccess) c->order_cap = size_t(1) << 18;
@@ -1816,12 +1843,23 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
 void rt4_context_destroy(rt4_context* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  if (ctx->launched) (void)hipEventSynchronize(ctx->done);  // frames in flight (side streams included)
   if (ctx->d_scene) (void)hipFree(ctx->d_scene);
   if (ctx->d_wlut) (void)hipFree(ctx->d_wlut);
   if (ctx->d_queue) (void)hipFree(ctx->d_queue);
   if (ctx->d_order) (void)hipFree(ctx->d_order);
   if (ctx->d_fcolor) (void)hipFree(ctx->d_fcolor);
   if (ctx->done) (void)hipEventDestroy(ctx->done);
+  for (int k = 0; k < 2; k++) {
+    if (ctx->side[k]) {
+      (void)hipStreamSynchronize(ctx->side[k]);
+      (void)hipStreamDestroy(ctx->side[k]);
+    }
+    if (ctx->traced[k]) (void)hipEventDestroy(ctx->traced[k]);
+    if (ctx->seq_done[k]) (void)hipEventDestroy(ctx->seq_done[k]);
+    if (ctx->d_ofcolor[k]) (void)hipFree(ctx->d_ofcolor[k]);
+  }
+  if (ctx->d_ocount) (void)hipFree(ctx->d_ocount);
   if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
   if (ctx->d_eval) (void)hipFree(ctx->d_eval);
   delete ctx;
@@ -1939,6 +1977,31 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
     }
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // Overlapped single frames: one image, one frame, a region the frame-colour pixel word
+  // holds; the trace goes to a side stream and its frame colours to a slot buffer, the fold to the caller's
+  // stream, so this frame's trace fills the GPU while the previous one drains.
+  const bool overlap = RT4_OVERLAP_FRAMES && !(ctx->flags & RT4_FLAG_SERIAL_FRAMES) && !frames && n_jobs == 1 &&
+                       a.jobs[0].reg.w <= 8191 && a.jobs[0].reg.h <= 8191;
+  const unsigned slot = ctx->launch_seq & 1u;
+  hipStream_t ts = s;  // the trace kernel's stream
+  if (overlap) {
+    const size_t need = static_cast<size_t>(a.jobs[0].reg.w) * static_cast<size_t>(a.jobs[0].reg.h) * sizeof(float4);
+    if (ctx->ofcolor_bytes < need) {  // the slots grow to the largest region seen (both idle first)
+      if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
+      for (int k = 0; k < 2; k++) {
+        if (ctx->side[k]) HIP_TRY(hipStreamSynchronize(ctx->side[k]));
+        if (ctx->d_ofcolor[k]) (void)hipFree(ctx->d_ofcolor[k]);
+        ctx->d_ofcolor[k] = nullptr;
+      }
+      ctx->ofcolor_bytes = 0;
+      for (int k = 0; k < 2; k++) HIP_TRY(hipMalloc(&ctx->d_ofcolor[k], need));
+      ctx->ofcolor_bytes = need;
+    }
+    if (!ctx->side[slot]) HIP_TRY(hipStreamCreateWithFlags(&ctx->side[slot], hipStreamNonBlocking));
+    ts = ctx->side[slot];
+    a.fcolor = static_cast<float4*>(ctx->d_ofcolor[slot]);
+    a.frame_part[0] = a.part;
+  }
   const Variant& v = variant_for(ctx->shape);
   const bool reuse = (ctx->flags & RT4_FLAG_PRIMARY_REUSE) && ctx->shape != GENERIC;
   const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0][reuse ? 1 : 0];
@@ -1959,7 +2022,10 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   if (reuse) a.eval_counter = ctx->d_eval;
   // The tile order buffer is one per context: a launch on another stream than the previous one
   // waits for it (launches of one context run in submission order).
-  if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(s, ctx->done, 0));
+  if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(ts, ctx->done, 0));
+  // launch s - 2 is complete before launch s starts: its queue word, frame-colour slot and count slot are
+  // free again (launch s - 1 may still be draining: that is the overlap)
+  HIP_TRY(hipStreamWaitEvent(ts, ctx->seq_done[slot], 0));
   if (frames) {  // the frame colours of a pipelined launch: one scratch buffer per context, grown to the
     // launch's frames (rt4_context_reserve_frames sizes it for a whole chunk ahead of time)
     const size_t need = static_cast<size_t>(fp->n) * static_cast<size_t>(a.jobs[0].reg.w) *
@@ -1978,7 +2044,7 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // Pipelined frames keep row-major order: the longest-first order only shortens the drain at the end
   // of a launch, which a pipelined launch pays once, and in the main phase row-major measured faster
   // (config 2 +1.5 %, config 3 +2 %; profiles/r02_ab.txt).
-  if (!frames) {
+  if (!frames && !overlap) {
   if (ctx->order_cap < tiles) {  // a frame larger than any before: grow once (allocates)
     HIP_TRY(hipStreamSynchronize(s));
     if (ctx->d_order) (void)hipFree(ctx->d_order);
@@ -2007,28 +2073,40 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   a.order_ends = ends;
   }
 #endif
+  // Queue words rotate; launch s zeroes launch s + 2's word (launch s + 1 may already be running, s + 2 starts
+  // only after s is complete): no memset between frames.
   unsigned* q = ctx->d_queue + (ctx->launch_seq % QUEUE_SLOTS);
-  unsigned* q_next = ctx->d_queue + (++ctx->launch_seq % QUEUE_SLOTS);  // zeroed by this launch
-  if (ctx->queue_dirty) {
-    HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), s));
+  unsigned* q_next = ctx->d_queue + ((ctx->launch_seq + 2u) % QUEUE_SLOTS);  // zeroed by this launch
+  const unsigned seq = ctx->launch_seq++;
+  if (ctx->queue_dirty && ctx->dirty_seq == seq) {
+    HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), ts));
     ctx->queue_dirty = false;
   }
+  unsigned long long* count = overlap ? ctx->d_ocount + slot : d_counter;
   (void)hipGetLastError();  // a sticky error of an earlier, unrelated call must not be taken for this launch's
-  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ctx->d_scene, scene_aux(ctx), a, d_counter,
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, ts, ctx->d_scene, scene_aux(ctx), a, count,
                      ctx->d_wlut, q, q_next);
   hipError_t le = hipGetLastError();
-  if (le == hipSuccess && frames) {
+  if (le == hipSuccess && overlap) {
+    le = hipEventRecord(ctx->traced[slot], ts);
+    if (le == hipSuccess) le = hipStreamWaitEvent(s, ctx->traced[slot], 0);
+  }
+  if (le == hipSuccess && (frames || overlap)) {
     const long long npx = static_cast<long long>(a.jobs[0].reg.w) * a.jobs[0].reg.h;
-    hipLaunchKernelGGL(rt4_fold_frames_kernel, dim3(static_cast<unsigned>((npx + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(rt4_fold_frames_kernel, dim3(static_cast<unsigned>((npx + 255) / 256)), dim3(256), 0, s, a,
+                       overlap ? count : nullptr, overlap ? d_counter : nullptr);
     le = hipGetLastError();
   }
-  // Record the event whatever happened: a launch that may have been enqueued still orders the next
+  // Record the events whatever happened: a launch that may have been enqueued still orders the next
   // launch on another stream behind it (they share d_order / the queue words).
-  const hipError_t re = hipEventRecord(ctx->done, s);
+  const hipError_t re2 = hipEventRecord(ctx->seq_done[slot], s);
+  hipError_t re = hipEventRecord(ctx->done, s);
+  if (re == hipSuccess) re = re2;
   ctx->last_stream = s;
   ctx->launched = true;
   if (le != hipSuccess) {
-    ctx->queue_dirty = true;  // q_next may not be zeroed
+    ctx->queue_dirty = true;  // q_next may not be zeroed: launch seq + 2 does it
+    ctx->dirty_seq = seq + 2u;
     rt4_set_err(err, errlen, "trace kernel launch failed: %s", hipGetErrorString(le));
     return RT4_ERR_HIP;
   }

@@ -76,6 +76,7 @@ SECTION_YXZ, SECTION_YWZ, SECTION_YXW = 0, 1, 2
 FLAG_SAMPLER_LUT = 0x1
 FLAG_GENERIC_KERNEL = 0x2
 FLAG_PRIMARY_REUSE = 0x4
+FLAG_SERIAL_FRAMES = 0x8
 FRAME_RGBA32F, FRAME_RGBA16F, FRAME_RGBA8 = 0, 1, 2
 KEY_FORWARD, KEY_BACK, KEY_RIGHT, KEY_LEFT, KEY_UP, KEY_DOWN, KEY_W_POS, KEY_W_NEG = (1 << i for i in range(8))
 MAX_SECTIONS = 3

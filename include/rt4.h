@@ -335,6 +335,13 @@ typedef struct rt4_context rt4_context;
  * actually evaluated. Specialised kernels only (ignored with RT4_FLAG_GENERIC_KERNEL or a generic
  * scene). SURVEY.md 8(d): a rate measured with it is labelled reference-equivalent. */
 #define RT4_FLAG_PRIMARY_REUSE 0x4u
+/* Single-frame launches (rt4_render_device[_ex], one-section rt4_render_sections_device) run entirely on
+ * the caller's stream. By default their trace kernel runs on one of two context-owned side streams and
+ * writes the frame's light sums to a slot buffer, and only the blend into the frame (and the count) runs on
+ * the caller's stream: back-to-back frames (a moving camera, main.cpp:93) then overlap each frame's trace with
+ * the previous frame's drain. Stream semantics are unchanged: the frame and the counter are written in the
+ * caller's stream order. Images are identical either way. */
+#define RT4_FLAG_SERIAL_FRAMES 0x8u
 
 int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err, size_t errlen);
 /* Uploads a scene (the reference recompiles the shader: src/main.cpp:25-39). Waits for the

@@ -405,3 +405,57 @@ def test_cpp_host_program_png(rt4, tmp_path):
     assert png[37:41] == b"IDAT"
     raw = zlib.decompress(png[41:41 + n])
     assert b"".join(raw[i * 289 + 1:(i + 1) * 289] for i in range(60)) == ppm
+
+
+@pytest.mark.parametrize("fmt", ["f32", "f16", "rgba8"])
+@pytest.mark.parametrize("name", ["sphere", "all_primitives"])
+def test_overlapped_frames_equal_serial(rt4, name, fmt):
+    """Single-frame launches overlap the previous frame's drain by default (rt4.h RT4_FLAG_SERIAL_FRAMES: the
+    trace on a side stream into a slot buffer, the blend and the count on the caller's stream).
+    A moving camera (new uniforms every frame, main.cpp:93), progressive parts, a pipelined call in between, a
+    frame on a second stream and a scene change: every frame and the count equal the serial launches bit for
+    bit after every step."""
+    import torch
+
+    f = FORMATS[fmt]
+    tdt = {0: torch.float32, 1: torch.float16, 2: torch.uint8}[f]
+    W, H = 131, 77
+    reg = rt4.region(W, H)
+    frames = [rt4.make_uniforms(W, H, samples=3, reflections=4, seed=40 + n, fi=5.0 * n, te=2.0 * n) for n in range(6)]
+    runs = []
+    for flags in (rt4.FLAG_SAMPLER_LUT, rt4.FLAG_SAMPLER_LUT | rt4.FLAG_SERIAL_FRAMES):
+        t = rt4.Tracer(device=0, flags=flags, scene=rt4.Scene.named(name))
+        out = []
+        try:
+            fr = torch.zeros((H, W, 4), dtype=tdt, device="cuda")
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            s = torch.cuda.current_stream()
+            for n, u in enumerate(frames[:3]):
+                t.render_device_ex(rt4.progressive_uniforms(u, n + 1), reg, fr.data_ptr(), f, W, cnt.data_ptr(),
+                                   s.cuda_stream)
+            out.append((fr.clone(), cnt.clone()))
+            t.reserve_frames(W, H)
+            t.render_frames_device([rt4.progressive_uniforms(frames[3], n) for n in (4, 5, 6)], reg, fr.data_ptr(), f,
+                                   W, cnt.data_ptr(), s.cuda_stream)
+            t.render_device_ex(rt4.progressive_uniforms(frames[4], 7), reg, fr.data_ptr(), f, W, cnt.data_ptr(),
+                               s.cuda_stream)
+            out.append((fr.clone(), cnt.clone()))
+            side = torch.cuda.Stream()
+            side.wait_stream(s)
+            t.render_device_ex(rt4.progressive_uniforms(frames[5], 8), reg, fr.data_ptr(), f, W, cnt.data_ptr(),
+                               side.cuda_stream)
+            s.wait_stream(side)
+            out.append((fr.clone(), cnt.clone()))
+            t.set_scene(rt4.Scene.named("hypercube"))
+            for n in range(2):
+                t.render_device_ex(rt4.progressive_uniforms(frames[n], 9 + n), reg, fr.data_ptr(), f, W, cnt.data_ptr(),
+                                   s.cuda_stream)
+            out.append((fr.clone(), cnt.clone()))
+            torch.cuda.synchronize()
+        finally:
+            t.close()
+        runs.append([(a.cpu().numpy(), int(c.item())) for a, c in out])
+    for step, ((a, na), (b, nb)) in enumerate(zip(*runs)):
+        assert na == nb, (step, na, nb)
+        eq = bits_equal(a, b)
+        assert eq.all(), f"step {step}: {(~eq).sum()} values differ"
