@@ -123,6 +123,10 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_OVERLAP_FRAMES
 #define RT4_OVERLAP_FRAMES 1  // single-frame launches overlap the previous frame's drain
 #endif
+#ifndef RT4_OVERLAP_SLOTS
+#define RT4_OVERLAP_SLOTS 3  // single-frame launches in flight at once (2..4; 3 measured best, profiles/r04_ab.txt)
+#endif
+static_assert(RT4_OVERLAP_SLOTS >= 2 && RT4_OVERLAP_SLOTS <= 4, "overlap slots");
 #ifndef RT4_WAVES_MIRROR
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
@@ -1397,15 +1401,16 @@ struct rt4_context {
   int n_cu = 0;
   TraceFn occ_fn = nullptr;  // blocks per CU of the last trace kernel launched (occupancy query cache)
   int occ_per_cu = 0;
-  // Overlapped single frames: launch s traces on side[s % 2] into ofcolor[s % 2] while
-  // launch s - 1 drains; its fold runs on the caller's stream. seq_done[s % 2]: recorded when launch s is
-  // complete (launch s + 2 waits for it: queue word, frame-colour and count slot).
-  hipStream_t side[2] = {nullptr, nullptr};
-  hipEvent_t traced[2] = {nullptr, nullptr};
-  hipEvent_t seq_done[2] = {nullptr, nullptr};
-  void* d_ofcolor[2] = {nullptr, nullptr};
+  // Overlapped single frames: launch s traces on side[s % S] into ofcolor[s % S] while
+  // launches s - S + 1 .. s - 1 drain (S = RT4_OVERLAP_SLOTS); its fold runs on the caller's stream.
+  // seq_done[s % S]: recorded when launch s is complete (launch s + S waits for it: queue word, frame-colour
+  // and count slot).
+  hipStream_t side[RT4_OVERLAP_SLOTS] = {};
+  hipEvent_t traced[RT4_OVERLAP_SLOTS] = {};
+  hipEvent_t seq_done[RT4_OVERLAP_SLOTS] = {};
+  void* d_ofcolor[RT4_OVERLAP_SLOTS] = {};
   size_t ofcolor_bytes = 0;      // bytes of each slot
-  unsigned long long* d_ocount = nullptr;  // 2 counters, one per slot
+  unsigned long long* d_ocount = nullptr;  // one counter per slot
 };
 
 #define HIP_TRY(expr)                                                                            \
@@ -1795,13 +1800,13 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
   if (e == hipSuccess) e = hipMemset(c->d_queue, 0, QUEUE_SLOTS * sizeof(unsigned));
   if (e == hipSuccess) e = hipDeviceSynchronize();  // zeroed before any stream's first launch
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
-  for (int k = 0; k < 2 && e == hipSuccess; k++) {
+  for (int k = 0; k < RT4_OVERLAP_SLOTS && e == hipSuccess; k++) {
     e = hipEventCreateWithFlags(&c->seq_done[k], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->traced[k], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(c->seq_done[k], nullptr);  // "launch -2 and -1" are complete
+    if (e == hipSuccess) e = hipEventRecord(c->seq_done[k], nullptr);  // "launches -S .. -1" are complete
   }
-  if (e == hipSuccess) e = hipMalloc(&c->d_ocount, 2 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemset(c->d_ocount, 0, 2 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&c->d_ocount, RT4_OVERLAP_SLOTS * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->d_ocount, 0, RT4_OVERLAP_SLOTS * sizeof(unsigned long long));
   if (e == hipSuccess) {  // tile order for frames up to 2^18 tiles (16.7 M pixels); larger ones grow it once
     e = hipMalloc(&c->d_order, ((size_t(1) << 18) + 2) * sizeof(unsigned));
     if (e == hipSuccess) c->order_cap = size_t(1) << 18;
@@ -1850,7 +1855,7 @@ void rt4_context_destroy(rt4_context* ctx) {
   if (ctx->d_order) (void)hipFree(ctx->d_order);
   if (ctx->d_fcolor) (void)hipFree(ctx->d_fcolor);
   if (ctx->done) (void)hipEventDestroy(ctx->done);
-  for (int k = 0; k < 2; k++) {
+  for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) {
     if (ctx->side[k]) {
       (void)hipStreamSynchronize(ctx->side[k]);
       (void)hipStreamDestroy(ctx->side[k]);
@@ -1982,19 +1987,19 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // stream, so this frame's trace fills the GPU while the previous one drains.
   const bool overlap = RT4_OVERLAP_FRAMES && !(ctx->flags & RT4_FLAG_SERIAL_FRAMES) && !frames && n_jobs == 1 &&
                        a.jobs[0].reg.w <= 8191 && a.jobs[0].reg.h <= 8191;
-  const unsigned slot = ctx->launch_seq & 1u;
+  const unsigned slot = ctx->launch_seq % RT4_OVERLAP_SLOTS;
   hipStream_t ts = s;  // the trace kernel's stream
   if (overlap) {
     const size_t need = static_cast<size_t>(a.jobs[0].reg.w) * static_cast<size_t>(a.jobs[0].reg.h) * sizeof(float4);
     if (ctx->ofcolor_bytes < need) {  // the slots grow to the largest region seen (both idle first)
       if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
-      for (int k = 0; k < 2; k++) {
+      for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) {
         if (ctx->side[k]) HIP_TRY(hipStreamSynchronize(ctx->side[k]));
         if (ctx->d_ofcolor[k]) (void)hipFree(ctx->d_ofcolor[k]);
         ctx->d_ofcolor[k] = nullptr;
       }
       ctx->ofcolor_bytes = 0;
-      for (int k = 0; k < 2; k++) HIP_TRY(hipMalloc(&ctx->d_ofcolor[k], need));
+      for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) HIP_TRY(hipMalloc(&ctx->d_ofcolor[k], need));
       ctx->ofcolor_bytes = need;
     }
     if (!ctx->side[slot]) HIP_TRY(hipStreamCreateWithFlags(&ctx->side[slot], hipStreamNonBlocking));
@@ -2023,8 +2028,8 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // The tile order buffer is one per context: a launch on another stream than the previous one
   // waits for it (launches of one context run in submission order).
   if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(ts, ctx->done, 0));
-  // launch s - 2 is complete before launch s starts: its queue word, frame-colour slot and count slot are
-  // free again (launch s - 1 may still be draining: that is the overlap)
+  // launch s - S is complete before launch s starts: its queue word, frame-colour slot and count slot are
+  // free again (launches s - S + 1 .. s - 1 may still be draining: that is the overlap)
   HIP_TRY(hipStreamWaitEvent(ts, ctx->seq_done[slot], 0));
   if (frames) {  // the frame colours of a pipelined launch: one scratch buffer per context, grown to the
     // launch's frames (rt4_context_reserve_frames sizes it for a whole chunk ahead of time)
@@ -2073,10 +2078,10 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   a.order_ends = ends;
   }
 #endif
-  // Queue words rotate; launch s zeroes launch s + 2's word (launch s + 1 may already be running, s + 2 starts
-  // only after s is complete): no memset between frames.
+  // Queue words rotate; launch s zeroes launch s + S's word (launches up to s + S - 1 may already be running,
+  // s + S starts only after s is complete): no memset between frames.
   unsigned* q = ctx->d_queue + (ctx->launch_seq % QUEUE_SLOTS);
-  unsigned* q_next = ctx->d_queue + ((ctx->launch_seq + 2u) % QUEUE_SLOTS);  // zeroed by this launch
+  unsigned* q_next = ctx->d_queue + ((ctx->launch_seq + RT4_OVERLAP_SLOTS) % QUEUE_SLOTS);  // zeroed by this launch
   const unsigned seq = ctx->launch_seq++;
   if (ctx->queue_dirty && ctx->dirty_seq == seq) {
     HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), ts));
@@ -2105,8 +2110,8 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   ctx->last_stream = s;
   ctx->launched = true;
   if (le != hipSuccess) {
-    ctx->queue_dirty = true;  // q_next may not be zeroed: launch seq + 2 does it
-    ctx->dirty_seq = seq + 2u;
+    ctx->queue_dirty = true;  // q_next may not be zeroed: launch seq + S does it
+    ctx->dirty_seq = seq + RT4_OVERLAP_SLOTS;
     rt4_set_err(err, errlen, "trace kernel launch failed: %s", hipGetErrorString(le));
     return RT4_ERR_HIP;
   }
