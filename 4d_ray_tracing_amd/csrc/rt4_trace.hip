@@ -120,6 +120,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
+#if defined(RT4_STAMPS) || defined(RT4_LANESTATS) || defined(RT4_TAILSTATS)
+#define RT4_OVERLAP_FRAMES 0  // the diagnostic builds write counter[1..]: the caller's buffer, never a count slot
+#endif
 #ifndef RT4_OVERLAP_FRAMES
 #define RT4_OVERLAP_FRAMES 1  // single-frame launches overlap the previous frame's drain
 #endif
