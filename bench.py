@@ -570,7 +570,9 @@ def main():
                 "peak": PEAK_FP32_VALU_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_VALU_TFLOPS,
-                "traffic": der.get("hbm_bytes_per_launch"),
+                # memory-side bytes per frame: request-counted where the profile has the pmc_req pass (exact for
+                # the table's 64-B requests), else FETCH_SIZE x 2 + WRITE_SIZE (an upper bound)
+                "traffic": der.get("traffic_bytes_per_launch", der.get("hbm_bytes_per_launch")),
                 "achieved_kind": "reference-equivalent: the reference's fp32 ops per unit (oracle op count, fma = 2) "
                                  "x units / kernel time; counts work the kernel skips exactly (tiger CSE, "
                                  "bounding-ball skips, the sampler table), so it is not a hardware utilisation",
@@ -596,11 +598,14 @@ def main():
                     f" (rocprofv3 PMC, {prof.get('frames_per_dispatch', 1)} frames per dispatch, per frame; trace "
                     f"{prof.get('avg_ns', 0) * 1e-6:.4f} ms per frame)")
             if prof and der.get("hbm_bytes_per_launch"):
-                line["roofline"]["traffic_source"] = src + " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per frame)"
+                exact = "traffic_bytes_per_launch" in der
+                line["roofline"]["traffic_source"] = src + (
+                    " (rocprofv3 TCC_EA0_RDREQ by request size + WRITE_SIZE, per frame)" if exact
+                    else " (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, per frame)")
                 if prof.get("avg_ns"):
                     # the north star's "achieved HBM GB/s": the profiled traffic over the profiled trace time per
                     # frame (memory-side bytes: the sampler gathers are served by the Infinity Cache)
-                    gbps = der["hbm_bytes_per_launch"] / prof["avg_ns"]
+                    gbps = line["roofline"]["traffic"] / prof["avg_ns"]
                     line["roofline"]["traffic_gbps"] = gbps
                     line["roofline"]["traffic_frac_of_hbm_peak"] = gbps / HBM_PEAK_GBPS
             if prof and der.get("fabric_read_requests") and prof.get("avg_ns"):

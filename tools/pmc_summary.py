@@ -91,6 +91,16 @@ def main():
     if "TCC_EA0_RDREQ_LEVEL_sum" in c and "TCC_EA0_RDREQ_sum" in c:
         # Little's law over the L2's fabric read interface (TCC cycles): the mean latency of an L2 miss
         m["ea_read_latency_cycles"] = c["TCC_EA0_RDREQ_LEVEL_sum"] / max(1.0, c["TCC_EA0_RDREQ_sum"])
+    if "TCC_EA0_RDREQ_32B_sum" in c and "TCC_BUBBLE_sum" in c and "TCC_EA0_RDREQ_sum" in c:
+        # request sizes (the FETCH_SIZE expression of rocprofv3 -L): 128 B bubbles, 32 B requests, 64 B the rest
+        r, r32, bub = c["TCC_EA0_RDREQ_sum"], c["TCC_EA0_RDREQ_32B_sum"], c["TCC_BUBBLE_sum"]
+        m["fabric_read_bytes"] = bub * 128 + (r - bub - r32) * 64 + r32 * 32
+        m["fabric_req_32b_share"] = r32 / max(1.0, r)
+        m["fabric_req_128b_share"] = bub / max(1.0, r)
+        if "hbm_write_bytes" in m:
+            # memory-side bytes of the launch from the request sizes (no gfx950 x2 correction: that one is for
+            # wide coalesced reads; these are 64-B requests, profiles/r04_ab.txt)
+            m["traffic_bytes_per_launch"] = m["fabric_read_bytes"] + m["hbm_write_bytes"]
     out["derived"] = m
     for log in ("trace.log", os.path.join("trace", "..", "bench.log")):
         lp = os.path.join(d, log)
@@ -106,7 +116,8 @@ def main():
                         out[k] /= fpl
                     for k in list(c):
                         c[k] /= fpl
-                    for k in ("hbm_read_bytes_corrected", "hbm_write_bytes", "hbm_bytes_per_launch", "fabric_read_requests"):
+                    for k in ("hbm_read_bytes_corrected", "hbm_write_bytes", "hbm_bytes_per_launch", "fabric_read_requests",
+                              "fabric_read_bytes", "traffic_bytes_per_launch"):
                         if k in m:
                             m[k] /= fpl
                 out["config"] = b["config"]

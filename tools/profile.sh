@@ -32,4 +32,6 @@ run pmc_tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_
 # mean fabric read latency (Little's law: requests in flight summed per cycle / requests), which tells an
 # Infinity-Cache-served gather (~545 cycles idle) from an HBM-served one (~900; MI355X_MICROARCH.md)
 run pmc_lat --kernel-trace --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum || true
+# request sizes of the fabric reads (FETCH_SIZE = 128 B x bubble + 64 B x the rest + 32 B x 32B requests)
+run pmc_req --kernel-trace --pmc TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_sum || true
 echo "profile $TAG done"
