@@ -571,7 +571,7 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
 
 // The exact tests of a lane's pending spheres in index order (pass 2 of find_cand), from the cull's dots
 // or the centre.
-template <uint32_t SH>
+template <uint32_t SH, bool GEO = true>
 __device__ __forceinline__ Cand exact_pending(const SceneAux* __restrict__ X, const PrimEntry* P, const Ray& ray,
                                               const SphereGeo& geo, uint32_t pend, Cand inter) {
   while (pend) {
@@ -586,7 +586,7 @@ __device__ __forceinline__ Cand exact_pending(const SceneAux* __restrict__ X, co
 #endif
     const int i = __builtin_ctz(pend);
     pend &= pend - 1u;
-    if constexpr (geo_spheres<SH>() > 0)
+    if constexpr (GEO && geo_spheres<SH>() > 0)
       inter = closest(sphere_exact_geo<SH>(X, P, geo, i), inter);
     else
       inter = closest(sphere_exact<SH>(X, P, ray, i), inter);

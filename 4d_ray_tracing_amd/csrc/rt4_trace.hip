@@ -126,6 +126,12 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_OVERLAP_FRAMES
 #define RT4_OVERLAP_FRAMES 1  // single-frame launches overlap the previous frame's drain
 #endif
+#ifndef RT4_DEFER_GEO
+#define RT4_DEFER_GEO 0  // the deferred-sphere kernel keeps the cull's dots for the exact tests (r03: 1)
+#endif
+#ifndef RT4_REFILL_ONE_TRIP
+#define RT4_REFILL_ONE_TRIP 1
+#endif
 #ifndef RT4_OVERLAP_SLOTS
 #define RT4_OVERLAP_SLOTS 3  // single-frame launches in flight at once (2..4; 3 measured best, profiles/r04_ab.txt)
 #endif
@@ -137,7 +143,7 @@ static_assert(RT4_OVERLAP_SLOTS >= 2 && RT4_OVERLAP_SLOTS <= 4, "overlap slots")
 #define RT4_WAVES_ALLPRIM 6  // tiger kernels with other groups (all_primitives: BASELINE config 5); r03-v40
 #endif
 #ifndef RT4_WAVES_SPHERE
-#define RT4_WAVES_SPHERE 6
+#define RT4_WAVES_SPHERE 7  // r04: 7 with the light sum in LDS and no kept cull dots (RT4_DEFER_GEO 0)
 #endif
 #ifndef RT4_WAVES_EXACT
 #define RT4_WAVES_EXACT 6  // exact-count kernels without a tiger (sphere, room, hypercube, cylinder4d): 6 waves/SIMD
@@ -419,15 +425,15 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
 // specialised for three or more spaces (the mirror room of
 // config 4) at 6 (+2.3 %); the one-space tiger kernel and everything else keep the allocator's choice
 // (a 6-wave bound costs the one-space tiger 1.2 %).
-constexpr int min_waves_of(uint32_t K) {
+constexpr int min_waves_of(uint32_t K, bool reuse = false) {
   if (K == GENERIC) return RT4_WAVES_PER_SIMD;
   if (!(K & K_TIGER)) {
     if ((K >> 8) == 0) return RT4_WAVES_PER_SIMD;  // runtime counts
-    // the one-space sphere kernel (BASELINE config 2): 6 waves since r03-v40 (80 VGPRs, 8 B/lane spill):
-    // with the deferred exact tests and four-tile claims it is 12 % faster than at 7 (72 VGPRs, where the
-    // claim state spilled 48 B/lane; profiles/r03_ab.txt); r02 had measured 7 +1-2.5 % over 6 without them.
+    // the one-space sphere kernel (BASELINE config 2): 7 waves since r04 (72 VGPRs, no spill in the loop) with
+    // its light sum in LDS and the exact tests recomputing the cull's dots: +3-4 % over r03-v40's 6 waves (80
+    // VGPRs), which had beaten 7 waves with the light sum in VGPRs (claim state spilled 48 B/lane; r03_ab.txt).
     // The hypercube kernel -1.3 % at 7 (profiles/r02_ab.txt)
-    if ((K & 0xFFu) == (K_SPACES | K_SPHERES) && ((K >> 8) & 0xFFu) == 2) return RT4_WAVES_SPHERE;
+    if ((K & 0xFFu) == (K_SPACES | K_SPHERES) && ((K >> 8) & 0xFFu) == 2) return reuse ? 6 : RT4_WAVES_SPHERE;
     return RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
   }
   if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return RT4_WAVES_ALLPRIM;
@@ -443,7 +449,7 @@ constexpr bool phase_refill_of(uint32_t K) {
 }
 
 template <uint32_t K, bool LUT, bool REUSE>
-__global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
+__global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         unsigned long long* __restrict__ counter,
                                                         const WEntry* __restrict__ wlut, unsigned* __restrict__ queue,
@@ -530,7 +536,10 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
   // in 4 VGPRs instead of cold[256], so the end of a sample is three register adds instead of an LDS
   // round trip. Measured (profiles/r02_ab.txt): sphere scene +1.2 %; the hypercube kernel -2.6 % (same
   // 6 waves/SIMD, worse allocation); the tiger kernels have no VGPRs to spare at their wave bounds.
-  constexpr bool LSUM_REG = RT4_LSUM_REG && K != GENERIC && !(K & (K_TIGER | K_HYPERCUBE));
+  // (not in the deferred-sphere kernel since r04: its light sum in LDS and the exact tests recomputing the
+  // cull's dots (DEFER_GEO) bring it to 72 VGPRs, 7 waves/SIMD with no spill in the loop: config 2 +3-4 %,
+  // profiles/r04_ab.txt)
+  constexpr bool LSUM_REG = RT4_LSUM_REG && K != GENERIC && !(K & (K_TIGER | K_HYPERCUBE)) && !(DEFER && !RT4_DEFER_GEO);
   float4 lsum_reg = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   auto lsum_load = [&]() -> float4 {
     if constexpr (LSUM_REG) return lsum_reg;
@@ -755,9 +764,16 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
           const unsigned n = min(nidle - got, 64u - in_next);
           if (!active && rank >= got && rank < got + n) {
             const unsigned e = wbase + in_next + (rank - got);
+            // both reads before the test: one LDS round trip per hand-out instead of two (RT4_REFILL_ONE_TRIP)
             const uint2 px = lds_in_px[e];
+#if RT4_REFILL_ONE_TRIP
+            const float4 d0 = lds_in_d0[e];
+            asm volatile("" ::"v"(d0.x), "v"(d0.y), "v"(d0.z), "v"(d0.w));  // keep the read here, beside px's
+#endif
             if (px.y != 0xFFFFFFFFu) {
+#if !RT4_REFILL_ONE_TRIP
               const float4 d0 = lds_in_d0[e];
+#endif
               rng = RngState{px.x, in_seed};
               ray = Ray{focus, V4{d0.x, d0.y, d0.z, d0.w}};
               acc = V3{0.0f, 0.0f, 0.0f};
@@ -899,7 +915,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       uint32_t pend = 0;
       SphereGeo geo;
       Cand inter = no_cand();
-      if (active) inter = find_pre<K>(S, X, ray, pend, &geo);
+      if (active) inter = find_pre<K>(S, X, ray, pend, RT4_DEFER_GEO ? &geo : nullptr);
       const unsigned long long pm = __ballot(pend != 0u);
       const bool run = pm != 0ull && (static_cast<unsigned>(__popcll(pm)) >= static_cast<unsigned>(RT4_DEFER_EXACT) ||
                                       defer_age >= RT4_DEFER_WAIT || pm == __ballot(active));
@@ -909,7 +925,7 @@ __global__ __launch_bounds__(256, min_waves_of(K)) void rt4_trace_kernel(const r
       } else {
         defer_age = 0;
       }
-      if (active && !parked) c = find_rest<K>(S, X, P, ray, exact_pending<K>(X, P, ray, geo, pend, inter));
+      if (active && !parked) c = find_rest<K>(S, X, P, ray, exact_pending<K, RT4_DEFER_GEO != 0>(X, P, ray, geo, pend, inter));
       RT4_ACC(1, t_ph);
     } else {
       if (!__any(active)) {
