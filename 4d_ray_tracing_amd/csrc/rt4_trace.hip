@@ -434,7 +434,7 @@ constexpr int min_waves_of(uint32_t K, bool reuse = false) {
     // VGPRs), which had beaten 7 waves with the light sum in VGPRs (claim state spilled 48 B/lane; r03_ab.txt).
     // The hypercube kernel -1.3 % at 7 (profiles/r02_ab.txt)
     if ((K & 0xFFu) == (K_SPACES | K_SPHERES) && ((K >> 8) & 0xFFu) == 2) return reuse ? 6 : RT4_WAVES_SPHERE;
-    return RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
+    return reuse ? 6 : RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
   }
   if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return RT4_WAVES_ALLPRIM;
   return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
