@@ -91,12 +91,22 @@ def unpermute(gathered, plan: BandPlan):
     if plan.world == 1:
         return gathered[0][: plan.height]
     flat = gathered.reshape((plan.world * plan.rows_max,) + tuple(gathered.shape[2:]))
-    idx = plan.gather_index()
-    if hasattr(flat, "index_select"):  # torch: one device copy
-        import torch
+    if hasattr(flat, "index_select"):  # torch: one device copy, the row index uploaded once per plan and device
+        return flat.index_select(0, _device_index(plan, flat.device))
+    return flat[plan.gather_index()]
 
-        return flat.index_select(0, torch.from_numpy(idx).to(flat.device))
-    return flat[idx]
+
+_INDEX_CACHE = {}
+_RECV_CACHE = {}
+
+
+def _device_index(plan: BandPlan, device):
+    import torch
+
+    key = (plan.width, plan.height, plan.world, plan.band, str(device))
+    if key not in _INDEX_CACHE:
+        _INDEX_CACHE[key] = torch.from_numpy(plan.gather_index()).to(device)
+    return _INDEX_CACHE[key]
 
 
 def gather_frame(local, plan: BandPlan, rank: int, group=None):
@@ -110,8 +120,14 @@ def gather_frame(local, plan: BandPlan, rank: int, group=None):
         return local
     if local.shape[0] != plan.rows_max:
         raise ValueError(f"shard has {local.shape[0]} rows, the plan gathers {plan.rows_max}")
-    bufs = [torch.empty_like(local) for _ in range(plan.world)] if rank == 0 else None
-    dist.gather(local, gather_list=bufs, dst=0, group=group)
+    recv = None
+    if rank == 0:  # one (world, rows_max, W, C) receive buffer, kept: the shards land in it without a stack copy
+        key = (plan.world,) + tuple(local.shape) + (local.dtype, str(local.device))
+        recv = _RECV_CACHE.get(key)
+        if recv is None:
+            recv = _RECV_CACHE[key] = torch.empty((plan.world,) + tuple(local.shape), dtype=local.dtype,
+                                                  device=local.device)
+    dist.gather(local, gather_list=list(recv.unbind(0)) if recv is not None else None, dst=0, group=group)
     if rank != 0:
         return None
-    return unpermute(torch.stack(bufs), plan)
+    return unpermute(recv, plan)
