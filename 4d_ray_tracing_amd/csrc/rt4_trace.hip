@@ -132,6 +132,19 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_REFILL_ONE_TRIP
 #define RT4_REFILL_ONE_TRIP 1
 #endif
+#ifndef RT4_OVERLAP_GRID_LESS
+// Overlapped traces of short frames (at most RT4_OVERLAP_SHORT_WORK pixel samples x (bounces + 1)) run this many
+// blocks per CU fewer than the occupancy allows, so that when one frame's trace holds the chip alone the previous
+// frame's fold finds free slots at once instead of waiting for that trace's drain (2 measured best: config 2
+// -9 %, config 3 -10 %; a long frame, config 4, loses 5 % with it; profiles/r04_ab.txt)
+#define RT4_OVERLAP_GRID_LESS 2
+#endif
+#ifndef RT4_OVERLAP_SHORT_WORK
+#define RT4_OVERLAP_SHORT_WORK (1ull << 30)
+#endif
+#ifndef RT4_SIDE_LOW_PRIORITY
+#define RT4_SIDE_LOW_PRIORITY 1  // overlapped traces on streams made with the least priority (measured 2-5 % faster)
+#endif
 #ifndef RT4_OVERLAP_SLOTS
 #define RT4_OVERLAP_SLOTS 3  // single-frame launches in flight at once (2..4; 3 measured best, profiles/r04_ab.txt)
 #endif
@@ -2021,7 +2034,15 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
       for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) HIP_TRY(hipMalloc(&ctx->d_ofcolor[k], need));
       ctx->ofcolor_bytes = need;
     }
-    if (!ctx->side[slot]) HIP_TRY(hipStreamCreateWithFlags(&ctx->side[slot], hipStreamNonBlocking));
+    if (!ctx->side[slot]) {
+      if (RT4_SIDE_LOW_PRIORITY) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&ctx->side[slot], hipStreamNonBlocking, least));
+      } else {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->side[slot], hipStreamNonBlocking));
+      }
+    }
     ts = ctx->side[slot];
     a.fcolor = static_cast<float4*>(ctx->d_ofcolor[slot]);
     a.frame_part[0] = a.part;
@@ -2037,7 +2058,11 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
     ctx->occ_per_cu = n;
   }
   const int per_cu = ctx->occ_per_cu;
-  long long blocks = static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1);
+  int bpc = per_cu > 0 ? per_cu : 1;
+  const unsigned long long frame_work = static_cast<unsigned long long>(a.total) * static_cast<unsigned>(a.samples) *
+                                       static_cast<unsigned>(a.reflections_amount + 1);
+  if (overlap && frame_work <= RT4_OVERLAP_SHORT_WORK) bpc = bpc > RT4_OVERLAP_GRID_LESS ? bpc - RT4_OVERLAP_GRID_LESS : 1;
+  long long blocks = static_cast<long long>(ctx->n_cu) * bpc;
   const long long items = static_cast<long long>(a.total >> 6);  // tiles of all jobs (and frames)
   if (blocks > (items + 3) / 4) blocks = (items + 3) / 4;  // >= one tile per wave
   if (blocks < 1) blocks = 1;
