@@ -327,6 +327,7 @@ struct JobArgs {
   int64_t row_stride_px;
   unsigned tile_base;  // first queue tile of the job (8x8 tiles, row-major inside the job)
   unsigned tiles_x;
+  unsigned fc_base;    // an overlapped sections launch: the section's first pixel in the frame-colour slot (else 0)
 };
 struct KernelArgs {
   // uniforms every job shares (one shader, one frame: rt4_check_jobs)
@@ -345,7 +346,7 @@ struct KernelArgs {
   // (frame_part[f]) into the frame buffer afterwards. Pixel words then pack j | i << 13 | f << 26.
   int32_t n_frames;
   unsigned frame_tiles;  // tiles per frame
-  float4* fcolor;        // n_frames x reg.h x reg.w; also set (n_frames 1) for an overlapped single frame
+  float4* fcolor;        // n_frames x reg.h x reg.w; also set (n_frames 1) for an overlapped launch: one image per section
   int32_t frame_seed[RT4_MAX_FRAMES];
   float frame_part[RT4_MAX_FRAMES];
 };
@@ -355,7 +356,8 @@ __device__ __forceinline__ int region_row(const rt4_region& r, int i) {
 }
 
 // A lane's pixel, packed into one dword of its cold state: region-local j (16 bits) | i (14) | job (2);
-// when the pixels go to the frame-colour scratch (KernelArgs::fcolor) j (13) | i (13) | frame (6).
+// when the pixels go to the frame-colour scratch (KernelArgs::fcolor) j (13) | i (13) | frame (6), where an overlapped
+// sections launch puts the section in the frame field.
 __device__ __forceinline__ int pack_pixel(int j, int i, int job) { return j | (i << 16) | (job << 30); }
 __device__ __forceinline__ int pack_pixel_f(int j, int i, int f) { return j | (i << 13) | (f << 26); }
 
@@ -611,8 +613,14 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
         // pipelined or overlapped frames: the light sum of frame f as is; rt4_fold_frames_kernel tone-maps and
         // blends
         const unsigned j = pk & 0x1FFF, i = (pk >> 13) & 0x1FFF, f = (pk >> 26) & 0x3F;  // < 2^28 pixels (4 GiB)
-        const rt4_region& rg = a.jobs[0].reg;
-        a.fcolor[(f * static_cast<unsigned>(rg.h) + i) * static_cast<unsigned>(rg.w) + j] = lp;
+        if (a.n_jobs == 1) {  // f: the frame of a pipelined launch
+          const rt4_region& rg = a.jobs[0].reg;
+          a.fcolor[(f * static_cast<unsigned>(rg.h) + i) * static_cast<unsigned>(rg.w) + j] = lp;
+        } else {  // f: the section of an overlapped sections launch
+          for (int jb = 0; jb < a.n_jobs; jb++)
+            if (f == static_cast<unsigned>(jb))
+              a.fcolor[a.jobs[jb].fc_base + i * static_cast<unsigned>(a.jobs[jb].reg.w) + j] = lp;
+        }
       } else {
         for (int jb = 0; jb < a.n_jobs; jb++)
           if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
@@ -680,7 +688,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
       dd = divs(dd, length(dd));
       d0 = make_float4(dd.x, dd.y, dd.z, dd.w);
       px = uint2{__float_as_uint(sx) ^ (__float_as_uint(sy) << 9) ^ in_seed,
-                 static_cast<uint32_t>(a.fcolor ? pack_pixel_f(jj, ii, static_cast<int>(frame)) : pack_pixel(jj, ii, job))};
+                 static_cast<uint32_t>(a.fcolor ? pack_pixel_f(jj, ii, static_cast<int>(frame) + job) : pack_pixel(jj, ii, job))};
     }
     lds_in_d0[threadIdx.x] = d0;
     lds_in_px[threadIdx.x] = px;
@@ -1248,9 +1256,10 @@ __global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, cons
 // count_src (an overlapped single frame): the trace kernel's count, moved into the caller's counter here, on
 // the caller's stream, and reset for the slot's next frame
 __global__ void rt4_fold_frames_kernel(const KernelArgs a, unsigned long long* count_src, unsigned long long* count_dst) {
-  const JobArgs& J = a.jobs[0];
+  const int job = static_cast<int>(blockIdx.y);  // the section of an overlapped sections launch (else 0)
+  const JobArgs& J = a.jobs[job];
   const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (count_src && p == 0) {
+  if (count_src && p == 0 && job == 0) {
     if (count_dst) atomicAdd(count_dst, *count_src);
     *count_src = 0ull;
   }
@@ -1260,7 +1269,7 @@ __global__ void rt4_fold_frames_kernel(const KernelArgs a, unsigned long long* c
   char* base = static_cast<char*>(J.frame);
   const int64_t at = static_cast<int64_t>(i) * J.row_stride_px + j;
   auto color = [&](int f) {  // frame f's light sum, tone-mapped as write_pixel does
-    const float4 l = a.fcolor[f * npx + p];
+    const float4 l = a.fcolor[J.fc_base + f * npx + p];
     return tone_map(a, V3{l.x, l.y, l.z});
   };
   if (a.format == RT4_FRAME_RGBA16F) {
@@ -2017,12 +2026,23 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // Overlapped single frames: one image, one frame, a region the frame-colour pixel word
   // holds; the trace goes to a side stream and its frame colours to a slot buffer, the fold to the caller's
   // stream, so this frame's trace fills the GPU while the previous one drains.
-  const bool overlap = RT4_OVERLAP_FRAMES && !(ctx->flags & RT4_FLAG_SERIAL_FRAMES) && !frames && n_jobs == 1 &&
-                       a.jobs[0].reg.w <= 8191 && a.jobs[0].reg.h <= 8191;
+  // Sections (rt4_render_sections_device, three_window_group.cpp:42-46) overlap too: the pixel word's frame field
+  // then names the section, and the slot buffer holds the sections' images one after another (JobArgs::fc_base).
+  bool small_regions = true;
+  size_t npx_all = 0;
+  for (int q = 0; q < n_jobs; q++) {
+    small_regions = small_regions && a.jobs[q].reg.w <= 8191 && a.jobs[q].reg.h <= 8191;
+    npx_all += static_cast<size_t>(a.jobs[q].reg.w) * static_cast<size_t>(a.jobs[q].reg.h);
+  }
+  const bool overlap = RT4_OVERLAP_FRAMES && !(ctx->flags & RT4_FLAG_SERIAL_FRAMES) && !frames && small_regions &&
+                       npx_all < (size_t(1) << 31);
+  if (overlap)
+    for (int q = 1; q < n_jobs; q++)
+      a.jobs[q].fc_base = a.jobs[q - 1].fc_base + static_cast<unsigned>(a.jobs[q - 1].reg.w) * static_cast<unsigned>(a.jobs[q - 1].reg.h);
   const unsigned slot = ctx->launch_seq % RT4_OVERLAP_SLOTS;
   hipStream_t ts = s;  // the trace kernel's stream
   if (overlap) {
-    const size_t need = static_cast<size_t>(a.jobs[0].reg.w) * static_cast<size_t>(a.jobs[0].reg.h) * sizeof(float4);
+    const size_t need = npx_all * sizeof(float4);
     if (ctx->ofcolor_bytes < need) {  // the slots grow to the largest region seen (both idle first)
       if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
       for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) {
@@ -2141,8 +2161,10 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
     if (le == hipSuccess) le = hipStreamWaitEvent(s, ctx->traced[slot], 0);
   }
   if (le == hipSuccess && (frames || overlap)) {
-    const long long npx = static_cast<long long>(a.jobs[0].reg.w) * a.jobs[0].reg.h;
-    hipLaunchKernelGGL(rt4_fold_frames_kernel, dim3(static_cast<unsigned>((npx + 255) / 256)), dim3(256), 0, s, a,
+    long long npx = 0;  // the largest image's pixels (blockIdx.y: the section)
+    for (int q = 0; q < n_jobs; q++) npx = std::max(npx, static_cast<long long>(a.jobs[q].reg.w) * a.jobs[q].reg.h);
+    hipLaunchKernelGGL(rt4_fold_frames_kernel, dim3(static_cast<unsigned>((npx + 255) / 256), static_cast<unsigned>(n_jobs)),
+                       dim3(256), 0, s, a,
                        overlap ? count : nullptr, overlap ? d_counter : nullptr);
     le = hipGetLastError();
   }

@@ -459,3 +459,48 @@ def test_overlapped_frames_equal_serial(rt4, name, fmt):
         assert na == nb, (step, na, nb)
         eq = bits_equal(a, b)
         assert eq.all(), f"step {step}: {(~eq).sum()} values differ"
+
+
+@pytest.mark.parametrize("fmt", ["f32", "rgba8"])
+@pytest.mark.parametrize("name", ["tiger", "sphere"])
+def test_overlapped_sections_equal_serial(rt4, name, fmt):
+    """Sections launches (three_window_group.cpp:42-46: YXZ at the main window's size, YWZ and YXW at the
+    additional one's) overlap like single frames: each section's image in its own part of the
+    slot buffer, one blend per section. A moving camera over progressive frames, with single-frame launches of a
+    larger region in between (the slot buffer grows and is shared): every image and the count equal the serial
+    launches bit for bit."""
+    import torch
+
+    f = FORMATS[fmt]
+    tdt = {0: torch.float32, 2: torch.uint8}[f]
+    sizes = [(121, 75), (60, 37), (60, 37)]
+    secs = (rt4.SECTION_YXZ, rt4.SECTION_YWZ, rt4.SECTION_YXW)
+    runs = []
+    for flags in (rt4.FLAG_SAMPLER_LUT, rt4.FLAG_SAMPLER_LUT | rt4.FLAG_SERIAL_FRAMES):
+        t = rt4.Tracer(device=0, flags=flags, scene=rt4.Scene.named(name))
+        out = []
+        try:
+            frames = [torch.zeros((h, w, 4), dtype=tdt, device="cuda") for (w, h) in sizes]
+            big = torch.zeros((90, 150, 4), dtype=tdt, device="cuda")
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            s = torch.cuda.current_stream().cuda_stream
+            for n in range(5):
+                jobs = []
+                for q, ((w, h), sec) in enumerate(zip(sizes, secs)):
+                    u = rt4.make_uniforms(w, h, samples=3, reflections=4, seed=90, section=sec, fi=20.0 + 4 * n,
+                                          te=10.0, psi=30.0)
+                    jobs.append((rt4.progressive_uniforms(u, n + 1), rt4.region(w, h), frames[q].data_ptr(), w))
+                t.render_sections_device(jobs, f, cnt.data_ptr(), s)
+                if n == 2:
+                    ub = rt4.make_uniforms(150, 90, samples=3, reflections=4, seed=91)
+                    t.render_device_ex(ub, rt4.region(150, 90), big.data_ptr(), f, 150, cnt.data_ptr(), s)
+                out.append([fr.clone() for fr in frames] + [big.clone(), cnt.clone()])
+            torch.cuda.synchronize()
+        finally:
+            t.close()
+        runs.append([[x.cpu().numpy() for x in step[:-1]] + [int(step[-1].item())] for step in out])
+    for n, (a, b) in enumerate(zip(*runs)):
+        assert a[-1] == b[-1], (n, a[-1], b[-1])
+        for q in range(4):
+            eq = bits_equal(a[q], b[q])
+            assert eq.all(), f"frame {n} image {q}: {(~eq).sum()} values differ"
