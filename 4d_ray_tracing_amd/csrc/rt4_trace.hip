@@ -146,9 +146,16 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #define RT4_SIDE_LOW_PRIORITY 1  // overlapped traces on streams made with the least priority (measured 2-5 % faster)
 #endif
 #ifndef RT4_OVERLAP_SLOTS
-#define RT4_OVERLAP_SLOTS 3  // single-frame launches in flight at once (2..4; 3 measured best, profiles/r04_ab.txt)
+// Overlapped launches in flight at once: RT4_OVERLAP_SLOTS (and as many side streams) for frames too small to fill
+// the chip, RT4_OVERLAP_BIG for the others (more streams than the process's four hardware queues cost a frame that
+// fills the chip 4-10 %; a small frame gains from every launch in flight; profiles/r04_ab.txt)
+#define RT4_OVERLAP_SLOTS 8
 #endif
-static_assert(RT4_OVERLAP_SLOTS >= 2 && RT4_OVERLAP_SLOTS <= 4, "overlap slots");
+#ifndef RT4_OVERLAP_BIG
+#define RT4_OVERLAP_BIG 3
+#endif
+static_assert(RT4_OVERLAP_SLOTS >= 2 && RT4_OVERLAP_SLOTS <= 8, "overlap slots");
+static_assert(RT4_OVERLAP_BIG >= 2 && RT4_OVERLAP_BIG <= RT4_OVERLAP_SLOTS, "overlap slots of big frames");
 #ifndef RT4_WAVES_MIRROR
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
@@ -2054,16 +2061,6 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
       for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) HIP_TRY(hipMalloc(&ctx->d_ofcolor[k], need));
       ctx->ofcolor_bytes = need;
     }
-    if (!ctx->side[slot]) {
-      if (RT4_SIDE_LOW_PRIORITY) {
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&ctx->side[slot], hipStreamNonBlocking, least));
-      } else {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->side[slot], hipStreamNonBlocking));
-      }
-    }
-    ts = ctx->side[slot];
     a.fcolor = static_cast<float4*>(ctx->d_ofcolor[slot]);
     a.frame_part[0] = a.part;
   }
@@ -2084,6 +2081,21 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   if (overlap && frame_work <= RT4_OVERLAP_SHORT_WORK) bpc = bpc > RT4_OVERLAP_GRID_LESS ? bpc - RT4_OVERLAP_GRID_LESS : 1;
   long long blocks = static_cast<long long>(ctx->n_cu) * bpc;
   const long long items = static_cast<long long>(a.total >> 6);  // tiles of all jobs (and frames)
+  // an overlapped frame with fewer tiles than the chip holds waves runs deep: up to RT4_OVERLAP_SLOTS in flight
+  const bool deep = overlap && items < static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1) * 4;
+  if (overlap) {
+    const unsigned sidx = ctx->launch_seq % (deep ? RT4_OVERLAP_SLOTS : RT4_OVERLAP_BIG);
+    if (!ctx->side[sidx]) {
+      if (RT4_SIDE_LOW_PRIORITY) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&ctx->side[sidx], hipStreamNonBlocking, least));
+      } else {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->side[sidx], hipStreamNonBlocking));
+      }
+    }
+    ts = ctx->side[sidx];
+  }
   if (blocks > (items + 3) / 4) blocks = (items + 3) / 4;  // >= one tile per wave
   if (blocks < 1) blocks = 1;
   a.order = nullptr;
@@ -2095,6 +2107,8 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // launch s - S is complete before launch s starts: its queue word, frame-colour slot and count slot are
   // free again (launches s - S + 1 .. s - 1 may still be draining: that is the overlap)
   HIP_TRY(hipStreamWaitEvent(ts, ctx->seq_done[slot], 0));
+  if (!deep && RT4_OVERLAP_BIG < RT4_OVERLAP_SLOTS)  // and launch s - RT4_OVERLAP_BIG (a frame that fills the chip)
+    HIP_TRY(hipStreamWaitEvent(ts, ctx->seq_done[(ctx->launch_seq + RT4_OVERLAP_SLOTS - RT4_OVERLAP_BIG) % RT4_OVERLAP_SLOTS], 0));
   if (frames) {  // the frame colours of a pipelined launch: one scratch buffer per context, grown to the
     // launch's frames (rt4_context_reserve_frames sizes it for a whole chunk ahead of time)
     const size_t need = static_cast<size_t>(fp->n) * static_cast<size_t>(a.jobs[0].reg.w) *
