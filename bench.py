@@ -93,6 +93,7 @@ def parse_args(argv=None):
                    help="RT4_FLAG_PRIMARY_REUSE for the main leg: value becomes reference-equivalent (labelled)")
     p.add_argument("--no-reuse-leg", action="store_true", help="skip the extra primary-reuse leg (N = 1)")
     p.add_argument("--no-fbf-leg", action="store_true", help="skip the extra frame-by-frame leg (N = 1)")
+    p.add_argument("--no-sections-leg", action="store_true", help="skip the extra 4D-view frame-loop leg (N = 1)")
     p.add_argument("--frame-by-frame", action="store_true",
                    help="one launch per frame (rt4_render_device_ex) instead of the pipelined frames of "
                         "rt4_render_frames_device (always so with a gather after every frame)")
@@ -246,6 +247,71 @@ def spawn_ranks(args):
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
 
+
+
+def sections_loop_leg(rt4, torch, gpu, flags, scene, stream, tracer, frames=40, warmup=10):
+    """Extra leg (N = 1): the reference's 4D view as its frame loop runs it (three_window_group.cpp:42-46, main.cpp:93):
+    three sections per frame at properties.txt's window cells (YXZ at the main window's, YWZ and YXW at the
+    additional one's), its samples and bounces, the bench's scene, a moving camera, one rt4_render_sections_device
+    call per frame. Timed with the launches overlapped (the default; on the bench's own context, as an application
+    with one context runs it) and with RT4_FLAG_SERIAL_FRAMES (a second context); the images and counts of the two
+    must agree bit for bit. Reported beside the headline, never as value."""
+    props = rt4.Properties(text=open(os.path.join(ROOT, "properties.txt")).read())
+    cells = [rt4.window_cells(props, "main"), rt4.window_cells(props, "additional"), rt4.window_cells(props, "additional")]
+    secs = [rt4.SECTION_YXZ, rt4.SECTION_YWZ, rt4.SECTION_YXW]
+    bases = [rt4.uniforms_from_properties(props, w, h, q) for (w, h), q in zip(cells, secs)]
+    sptr = stream.cuda_stream
+    out, images = {}, {}
+    for label, fl in (("overlapped", flags), ("serial", flags | rt4.FLAG_SERIAL_FRAMES)):
+        t = tracer if label == "overlapped" else rt4.Tracer(device=gpu, flags=fl, scene=scene)
+        try:
+            cam = rt4.Camera(props)
+            imgs = [torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{gpu}") for (w, h) in cells]
+            cnt = torch.zeros(1, dtype=torch.int64, device=f"cuda:{gpu}")
+
+            plan = []  # the camera path first (it does not depend on the frames), so the timed loop only submits
+            for n in range(warmup + frames):
+                fn = cam.s.frame_number
+                jobs = []
+                for q in range(3):
+                    cam.s.frame_number = fn
+                    jobs.append((cam.frame_uniforms(bases[q], secs[q], 4242 + n), rt4.region(*cells[q]),
+                                 imgs[q].data_ptr(), cells[q][0]))
+                plan.append(jobs)
+                cam.move(rt4.KEY_FORWARD, 0.01)
+
+            def frame(n):
+                t.render_sections_device(plan[n], rt4.FRAME_RGBA32F, cnt.data_ptr(), sptr)
+
+            for n in range(warmup):
+                frame(n)
+            torch.cuda.synchronize()
+            cnt.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(stream)
+            for n in range(frames):
+                frame(warmup + n)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            n_int = int(cnt.item())
+            out[label] = {"ms_per_frame": el / frames * 1e3, "kernel_ms_per_frame": e0.elapsed_time(e1) / frames,
+                          "value": n_int / el, "intersections_per_frame": n_int / frames}
+            images[label] = [x.cpu().numpy() for x in imgs]
+        finally:
+            if t is not tracer:
+                t.close()
+    same = all((a.view("u4") == b.view("u4")).all() for a, b in zip(images["overlapped"], images["serial"]))
+    same = same and out["overlapped"]["intersections_per_frame"] == out["serial"]["intersections_per_frame"]
+    if not same:
+        raise SystemExit("sections leg: overlapped and serial launches differ")
+    return {"label": "the 4D view's frame loop: three sections per frame at properties.txt's cells "
+                     f"({cells[0][0]}x{cells[0][1]}, 2x {cells[1][0]}x{cells[1][1]}), {bases[0].samples} spp, "
+                     f"{bases[0].reflections_amount} bounces, a moving camera, one rt4_render_sections_device call "
+                     "per frame; overlapped launches (default) against RT4_FLAG_SERIAL_FRAMES, same images and count",
+            "frames": frames, "unit": "ray-bounce intersections/s", **out,
+            "speedup": out["serial"]["ms_per_frame"] / out["overlapped"]["ms_per_frame"]}
 
 def main():
     args = parse_args()
@@ -493,6 +559,9 @@ def main():
             "intersections_per_step": n_r / args.steps, "evaluated_per_step": t_r.evaluated() / args.steps,
         }
         t_r.close()
+    sections_leg = None
+    if world == 1 and not args.no_sections_leg:
+        sections_leg = sections_loop_leg(rt4, torch, gpu, flags, scene, stream, tracer)
     if world > 1:
         st = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
@@ -558,6 +627,8 @@ def main():
             line["primary_reuse_leg"] = reuse_leg
         if fbf_leg:
             line["frame_by_frame_leg"] = fbf_leg
+        if sections_leg:
+            line["sections_loop_leg"] = sections_leg
         if strong:
             line["t1_ms"] = t1_ms if world > 1 else ms_per_step
             line["efficiency"] = (line["t1_ms"] / (world * ms_per_step)) if line["t1_ms"] else None

@@ -34,6 +34,11 @@ def test_bench_json_line():
     assert 0 < rf["frac"] < 1 and rf["peak"] == 157.3 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"])
     assert rf["ops_per_unit_executed"] < rf["ops_per_unit"] and rf["frac_executed"] < rf["frac"]
     assert d["setup_ms"]["set_scene_repeat_ms"] < d["setup_ms"]["set_scene_ms"] + 1.0
+    # the 4D view's frame loop at properties.txt's sizes: overlapped launches against serial ones (bench.py
+    # refuses to print a line when their images or counts differ); small frames gain the most
+    sl = d["sections_loop_leg"]
+    assert sl["overlapped"]["intersections_per_frame"] == sl["serial"]["intersections_per_frame"] > 0
+    assert sl["speedup"] > 1.5
 
 
 def test_bench_strong_config4_one_gpu():
