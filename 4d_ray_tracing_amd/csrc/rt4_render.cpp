@@ -254,6 +254,9 @@ uint32_t keys_from(const char* s) {  // controls.cpp:98-113 key names
 }  // namespace
 
 int main(int argc, char** argv) {
+  // The frame loop's overlapped launches of small frames use up to 8 side streams: give the
+  // process 8 hardware queues unless the environment says otherwise (read when the HIP runtime starts).
+  setenv("GPU_MAX_HW_QUEUES", "8", 0);
   std::string props_path = "properties.txt", scene_arg, out = "frame", fmt_name = "f32";
   int frames = 1, device = 0, width = 0, height = 0;
   bool three = false, frame_by_frame = false;
