@@ -98,3 +98,13 @@ def test_committed_profiles_cover_every_config_of_the_current_kernel(rt4):
 def test_gather_ceiling_is_the_committed_probe():
     """roofline.gather_rate_frac divides by the measured 32 MiB random-gather ceiling (profiles/r03_mall)."""
     assert abs(bench.gather_ceiling() - 65.69e9) < 1e6
+
+
+def test_bench_gives_its_process_eight_hardware_queues():
+    """bench.py sets GPU_MAX_HW_QUEUES for its own process before the HIP runtime starts (the overlapped small
+    frames' 8 side streams); --hw-queues 0 keeps the environment's value."""
+    assert bench.parse_args([]).hw_queues == 8
+    assert bench.parse_args(["--hw-queues", "0"]).hw_queues == 0
+    src = open(bench.__file__).read()
+    main = src[src.index("def main():"):]
+    assert main.index('os.environ["GPU_MAX_HW_QUEUES"]') < main.index("import torch")
