@@ -503,7 +503,11 @@ __device__ __forceinline__ Cand find_pre(const rt4_scene_desc* __restrict__ S, c
         }
       }
       const bool outside = d2 >= k[4];  // len_po >= max(r, SMALL)
+#ifdef RT4_CULL_BITWISE  // A/B build only: the same predicate without short-circuit branches
+      const bool skip = outside & ((dp < 0.0f) | (d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5])));
+#else
       const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5]));
+#endif
       pend |= skip ? 0u : (1u << i);
     });
   }

@@ -156,11 +156,24 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #endif
 static_assert(RT4_OVERLAP_SLOTS >= 2 && RT4_OVERLAP_SLOTS <= 8, "overlap slots");
 static_assert(RT4_OVERLAP_BIG >= 2 && RT4_OVERLAP_BIG <= RT4_OVERLAP_SLOTS, "overlap slots of big frames");
+// Wave bounds keep every trace kernel off scratch inside its trace loop (checked on the built
+// library by tools/codegen_check.py and tests/test_codegen.py). At 6 waves/SIMD the tiger kernels ran at the
+// register limit, spilling path state in the loop, and there the compiler's live-range splitting could put
+// register copies ahead of a join block's EXEC restore: the lanes the restore re-enables skip the copy-out but
+// run the copy-back, and receive another variable's value (the intersection count, the light sum's pixel word).
+// Which build hit it depended on scheduling: the -amdgpu-sched-strategy=iterative-ilp build and a build with the
+// sphere cull's && / || written as & / | computed other images and counts; the shipped one did not, by luck.
 #ifndef RT4_WAVES_MIRROR
-#define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
+#define RT4_WAVES_MIRROR 5  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
 #ifndef RT4_WAVES_ALLPRIM
-#define RT4_WAVES_ALLPRIM 6  // tiger kernels with other groups (all_primitives: BASELINE config 5); r03-v40
+#define RT4_WAVES_ALLPRIM 5  // tiger kernels with other groups (all_primitives: BASELINE config 5)
+#endif
+#ifndef RT4_WAVES_ALLPRIM_REUSE
+#define RT4_WAVES_ALLPRIM_REUSE 4  // their primary-reuse instantiations (96 VGPRs at 5 still spilled)
+#endif
+#ifndef RT4_WAVES_UNION_REUSE
+#define RT4_WAVES_UNION_REUSE 5  // the cylinders-union kernel's primary-reuse instantiation (spilled at 6)
 #endif
 #ifndef RT4_WAVES_SPHERE
 #define RT4_WAVES_SPHERE 7  // r04: 7 with the light sum in LDS and no kept cull dots (RT4_DEFER_GEO 0)
@@ -456,9 +469,10 @@ constexpr int min_waves_of(uint32_t K, bool reuse = false) {
     // VGPRs), which had beaten 7 waves with the light sum in VGPRs (claim state spilled 48 B/lane; r03_ab.txt).
     // The hypercube kernel -1.3 % at 7 (profiles/r02_ab.txt)
     if ((K & 0xFFu) == (K_SPACES | K_SPHERES) && ((K >> 8) & 0xFFu) == 2) return reuse ? 6 : RT4_WAVES_SPHERE;
+    if (reuse && (K & K_UNION)) return RT4_WAVES_UNION_REUSE;
     return reuse ? 6 : RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
   }
-  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return RT4_WAVES_ALLPRIM;
+  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return reuse ? RT4_WAVES_ALLPRIM_REUSE : RT4_WAVES_ALLPRIM;
   return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
 }
 
@@ -616,6 +630,13 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
     if (lane < ring_n) {
       const float4 lp = lds_out[wbase + lane];
       const int pk = __float_as_int(lp.w);
+#ifdef RT4_GUARD_WRITES  // diagnostic builds only (tools/variant_probe.py): drop a pixel word outside the launch
+      const unsigned gj = a.fcolor ? pk & 0x1FFF : pk & 0xFFFF, gi = a.fcolor ? (pk >> 13) & 0x1FFF : (pk >> 16) & 0x3FFF;
+      const unsigned gq = a.fcolor ? (pk >> 26) & 0x3F : (pk >> 30) & 3;
+      const unsigned gn = a.fcolor && a.n_jobs == 1 ? static_cast<unsigned>(a.n_frames) : static_cast<unsigned>(a.n_jobs);
+      const rt4_region& grg = a.jobs[gq < static_cast<unsigned>(a.n_jobs) ? gq : 0].reg;
+      if (gq < gn && gj < static_cast<unsigned>(grg.w) && gi < static_cast<unsigned>(grg.h))
+#endif
       if (a.fcolor) {
         // pipelined or overlapped frames: the light sum of frame f as is; rt4_fold_frames_kernel tone-maps and
         // blends
