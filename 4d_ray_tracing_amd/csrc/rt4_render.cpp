@@ -24,6 +24,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -112,11 +113,15 @@ class Agreement {
 // context, stream and buffers on device 0, and each rank copies its shard into its slot of rank 0's
 // gathered buffer with hipMemcpyAsync where the real run calls ncclGather; the band plan, the barrier,
 // the agreements and the un-permute are the real ones. fail_rank >= 0 (the RT4_RENDER_FAIL_RANK test hook)
-// makes that rank's set-up fail after its allocations, to exercise the error path.
+// makes that rank's set-up fail after its allocations, or with fail_gather (RT4_RENDER_FAIL_STAGE=gather) its
+// gather: the rank does not enqueue its part of the collective and reports an error, as when ncclGather fails.
+// After the gather is enqueued the ranks agree once more: if any rank failed, every rank aborts its communicator
+// (ncclCommAbort), so no rank waits forever in a collective its peer never joined. While the gather runs, every
+// rank also watches its communicator's asynchronous error (ncclCommGetAsyncError) and a shared abort flag.
 // Returns the frame on the host (rank 0's), or exits with status 1 naming the failed rank(s).
 std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc* scene, const std::vector<rt4_uniforms>& us,
                                         int32_t w, int32_t h, int32_t format, bool frame_by_frame, bool rehearse,
-                                        int fail_rank, unsigned long long* count_out, double* ms_out) {
+                                        int fail_rank, bool fail_gather, unsigned long long* count_out, double* ms_out) {
   const int32_t px = rt4_frame_format_bytes(format);
   std::vector<ncclComm_t> comms(static_cast<size_t>(gpus), nullptr);
   if (!rehearse) {
@@ -129,6 +134,7 @@ std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc
   Barrier bar(gpus);
   Agreement agree(gpus, bar);
   void* root_gathered = nullptr;  // rank 0's gathered buffer (rehearse: the other ranks copy into it)
+  std::atomic<bool> abort_all{false};  // a rank saw its communicator fail: every rank aborts its own
   auto rank_main = [&](int r) {
     BandRun& run = runs[static_cast<size_t>(r)];
     char err[1024] = {0};
@@ -161,7 +167,7 @@ std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc
     const bool pipelined = ok && !frame_by_frame && us.size() >= 2 && reg.h > 0 &&
                            rt4_context_frames_per_launch(ctx, reg.w, reg.h) > 1;
     if (ok && pipelined && rt4_context_reserve_frames(ctx, reg.w, reg.h, err, sizeof err) != RT4_OK) ok = fail(err);
-    if (ok && r == fail_rank) ok = fail("set-up failure injected (RT4_RENDER_FAIL_RANK)");
+    if (ok && r == fail_rank && !fail_gather) ok = fail("set-up failure injected (RT4_RENDER_FAIL_RANK)");
     if (ok) ok = hipDeviceSynchronize() == hipSuccess || fail("hipDeviceSynchronize");
     if (r == 0) root_gathered = gathered;  // read by the other ranks only after the agreement's barrier
     // every rank set up (the agreement is also the start barrier): otherwise nobody renders or gathers
@@ -180,24 +186,50 @@ std::vector<unsigned char> render_bands(int gpus, int band, const rt4_scene_desc
     }
     // the renders were enqueued everywhere: only then the collective (a launch error skips it on every rank)
     const bool all_rendered = all_set && agree.all(r, ok);
+    bool all_gathered = false;
     if (all_rendered) {
-      if (rehearse) {
+      ncclComm_t comm = rehearse ? nullptr : comms[static_cast<size_t>(r)];
+      if (r == fail_rank && fail_gather) {
+        ok = fail(rehearse ? "rehearsal gather copy failure injected (RT4_RENDER_FAIL_STAGE=gather)"
+                           : "ncclGather failure injected (RT4_RENDER_FAIL_STAGE=gather)");
+      } else if (rehearse) {
         ok = (hipMemcpyAsync(static_cast<char*>(root_gathered) + static_cast<size_t>(r) * shard_bytes, shard, shard_bytes,
                              hipMemcpyDeviceToDevice, stream) == hipSuccess &&
               hipStreamSynchronize(stream) == hipSuccess) ||
              fail("rehearsal gather copy");
-        bar.wait();  // every shard is in rank 0's buffer before the un-permute
-      } else if (ncclGather(shard, gathered, shard_bytes, ncclUint8, 0, comms[static_cast<size_t>(r)], stream) !=
-                 ncclSuccess) {
+      } else if (ncclGather(shard, gathered, shard_bytes, ncclUint8, 0, comm, stream) != ncclSuccess) {
         ok = fail("ncclGather failed");
       }
-      if (ok && r == 0 &&
+      // every rank enqueued its part (rehearse: every shard is in rank 0's buffer): otherwise the ranks that did
+      // wait for a peer that never joins, so every rank aborts its communicator instead of synchronising
+      all_gathered = agree.all(r, ok);
+      if (!all_gathered) {
+        abort_all = true;
+      } else if (!rehearse) {
+        // the gather runs: watch the communicator (an asynchronous error on any rank aborts them all)
+        hipError_t q;
+        while ((q = hipStreamQuery(stream)) == hipErrorNotReady && !abort_all) {
+          ncclResult_t ae = ncclSuccess;
+          if (ncclCommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess) {
+            ok = fail("RCCL asynchronous error in ncclGather");
+            abort_all = true;
+          }
+          std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+        if (q != hipSuccess && q != hipErrorNotReady) ok = fail("hipStreamQuery after ncclGather");
+      }
+      if (abort_all && comm) {
+        (void)ncclCommAbort(comm);  // returns the pending collective; the communicator is gone
+        comms[static_cast<size_t>(r)] = nullptr;
+        if (ok) ok = fail("communicator aborted: another rank failed in the gather");
+      }
+      if (ok && !abort_all && r == 0 &&
           rt4_bands_unpermute_device(gathered, img, w, h, gpus, band, rows_max, format, stream, err, sizeof err) != RT4_OK)
         ok = fail(err);
     }
-    if (stream && hipStreamSynchronize(stream) != hipSuccess) ok = fail("hipStreamSynchronize");
+    if (stream && hipStreamSynchronize(stream) != hipSuccess && !abort_all) ok = fail("hipStreamSynchronize");
     run.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (!all_rendered && ok) fail("skipped: another rank failed");
+    if ((!all_rendered || !all_gathered) && ok) fail("skipped: another rank failed");
     if (ok && hipMemcpy(&run.count, d_count, sizeof run.count, hipMemcpyDeviceToHost) != hipSuccess) fail("count");
     if (ok && r == 0 && hipMemcpy(image.data(), img, image.size(), hipMemcpyDeviceToHost) != hipSuccess)
       fail("image copy");
@@ -369,8 +401,10 @@ int main(int argc, char** argv) {
       HIP_CHECK(hipGetDeviceCount(&ndev));
       if (gpus > ndev) die("--gpus", ("only " + std::to_string(ndev) + " HIP devices").c_str());
     }
-    const char* fail_env = std::getenv("RT4_RENDER_FAIL_RANK");  // test hook: this rank's set-up fails
+    const char* fail_env = std::getenv("RT4_RENDER_FAIL_RANK");  // test hook: this rank's set-up fails,
     const int fail_rank = fail_env ? std::atoi(fail_env) : -1;
+    const char* stage_env = std::getenv("RT4_RENDER_FAIL_STAGE");  // or with "gather" its part of the gather
+    const bool fail_gather = stage_env && std::strcmp(stage_env, "gather") == 0;
     std::vector<rt4_uniforms> us;
     for (int n = 1; n <= frames; n++) {
       rt4_uniforms u;
@@ -381,7 +415,8 @@ int main(int argc, char** argv) {
     unsigned long long count = 0;
     double ms = 0.0;
     const std::vector<unsigned char> img =
-        render_bands(gpus, band, scene, us, cw[0], ch[0], format, frame_by_frame, rehearse, fail_rank, &count, &ms);
+        render_bands(gpus, band, scene, us, cw[0], ch[0], format, frame_by_frame, rehearse, fail_rank, fail_gather, &count,
+                     &ms);
     const std::string path = out + (png ? "_yxz.png" : "_yxz.ppm");
     RT4_CHECK((png ? rt4_write_png : rt4_write_ppm)(path.c_str(), img.data(), format, cw[0], ch[0], cw[0], err, sizeof err));
     if (raw) write_raw(out + "_yxz.raw", img);

@@ -1464,21 +1464,24 @@ struct rt4_context {
   hipStream_t last_stream = nullptr;
   bool launched = false;
   unsigned launch_seq = 0;
-  bool queue_dirty = false;  // a launch failed: launch dirty_seq zeroes its queue word itself
-  unsigned dirty_seq = 0;
+  bool q_dirty[QUEUE_SLOTS] = {};  // a launch failed before zeroing this queue word: its next user zeroes it
   unsigned long long* d_eval = nullptr;  // evaluated find calls (RT4_FLAG_PRIMARY_REUSE), rt4_context_evaluated
   int n_cu = 0;
   TraceFn occ_fn = nullptr;  // blocks per CU of the last trace kernel launched (occupancy query cache)
   int occ_per_cu = 0;
-  // Overlapped single frames: launch s traces on side[s % S] into ofcolor[s % S] while
-  // launches s - S + 1 .. s - 1 drain (S = RT4_OVERLAP_SLOTS); its fold runs on the caller's stream.
-  // seq_done[s % S]: recorded when launch s is complete (launch s + S waits for it: queue word, frame-colour
-  // and count slot).
+  // Overlapped single frames: launch s traces on a side stream into a slot buffer while the
+  // launches before it drain; its fold runs on the caller's stream. A frame too small to fill the chip ("deep")
+  // runs up to S = RT4_OVERLAP_SLOTS in flight (side stream and buffer s % S), any other frame up to
+  // B = RT4_OVERLAP_BIG (side stream and buffer s % B), so a frame that fills the chip allocates only B buffers.
+  // seq_done[s % S]: recorded when launch s is complete (launch s + S, and for a big frame s + B, waits for it:
+  // queue word, frame-colour buffer and count slot). Switching between deep and big frames first drains every
+  // launch in flight (the two buffer rotations share buffers 0 .. B - 1).
   hipStream_t side[RT4_OVERLAP_SLOTS] = {};
   hipEvent_t traced[RT4_OVERLAP_SLOTS] = {};
   hipEvent_t seq_done[RT4_OVERLAP_SLOTS] = {};
   void* d_ofcolor[RT4_OVERLAP_SLOTS] = {};
-  size_t ofcolor_bytes = 0;      // bytes of each slot
+  size_t ofcolor_cap[RT4_OVERLAP_SLOTS] = {};  // bytes of each slot buffer (grown to the largest launch it served)
+  bool overlapped = false, last_deep = false;  // the last overlapped launch's rotation
   unsigned long long* d_ocount = nullptr;  // one counter per slot
 };
 
@@ -1990,6 +1993,51 @@ struct FramePlan {
   const float* parts;
 };
 
+// The trace kernel a launch of the context runs: its scene's shape, the sampler table, primary reuse.
+TraceFn trace_fn_of(const rt4_context* ctx) {
+  const bool reuse = (ctx->flags & RT4_FLAG_PRIMARY_REUSE) && ctx->shape != GENERIC;
+  return variant_for(ctx->shape).trace[ctx->d_wlut ? 1 : 0][reuse ? 1 : 0];
+}
+
+// Blocks per CU the trace kernel fn holds (occupancy query, cached per kernel).
+int occupancy_of(rt4_context* ctx, TraceFn fn, int* per_cu, char* err, size_t errlen) {
+  if (ctx->occ_fn != fn) {
+    int n = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), 256, 0));
+    ctx->occ_fn = fn;
+    ctx->occ_per_cu = n;
+  }
+  *per_cu = ctx->occ_per_cu;
+  return RT4_OK;
+}
+
+// An overlapped launch of `items` 8x8 tiles runs deep (RT4_OVERLAP_SLOTS in flight) when it has fewer tiles than
+// the chip holds waves, unless the context caps the overlap (RT4_FLAG_OVERLAP_SHALLOW).
+bool overlap_deep(const rt4_context* ctx, long long items, int per_cu) {
+  if (ctx->flags & RT4_FLAG_OVERLAP_SHALLOW) return false;
+  return items < static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1) * 4;
+}
+
+// Slot buffer k holds at least `need` bytes. Growing it first waits for every launch in flight (a buffer may be
+// in use by any of them). kSlotNoMem when the allocation fails (the caller then runs the frame serially).
+constexpr int kSlotNoMem = 1;
+int ensure_overlap_buffer(rt4_context* ctx, unsigned k, size_t need, char* err, size_t errlen) {
+  if (ctx->ofcolor_cap[k] >= need) return RT4_OK;
+  if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
+  for (int q = 0; q < RT4_OVERLAP_SLOTS; q++)
+    if (ctx->side[q]) HIP_TRY(hipStreamSynchronize(ctx->side[q]));
+  if (ctx->d_ofcolor[k]) (void)hipFree(ctx->d_ofcolor[k]);
+  ctx->d_ofcolor[k] = nullptr;
+  ctx->ofcolor_cap[k] = 0;
+  if (hipMalloc(&ctx->d_ofcolor[k], need) != hipSuccess) {
+    (void)hipGetLastError();  // not sticky for the launch that follows
+    ctx->d_ofcolor[k] = nullptr;
+    return kSlotNoMem;
+  }
+  ctx->ofcolor_cap[k] = need;
+  return RT4_OK;
+}
+
 int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, int32_t format,
                 unsigned long long* d_counter, void* stream, char* err, size_t errlen, const FramePlan* fp = nullptr) {
   if (!ctx || !jobs) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
@@ -2062,48 +2110,39 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
     small_regions = small_regions && a.jobs[q].reg.w <= 8191 && a.jobs[q].reg.h <= 8191;
     npx_all += static_cast<size_t>(a.jobs[q].reg.w) * static_cast<size_t>(a.jobs[q].reg.h);
   }
-  const bool overlap = RT4_OVERLAP_FRAMES && !(ctx->flags & RT4_FLAG_SERIAL_FRAMES) && !frames && small_regions &&
-                       npx_all < (size_t(1) << 31);
-  if (overlap)
-    for (int q = 1; q < n_jobs; q++)
-      a.jobs[q].fc_base = a.jobs[q - 1].fc_base + static_cast<unsigned>(a.jobs[q - 1].reg.w) * static_cast<unsigned>(a.jobs[q - 1].reg.h);
+  bool overlap = RT4_OVERLAP_FRAMES && !(ctx->flags & RT4_FLAG_SERIAL_FRAMES) && !frames && small_regions &&
+                 npx_all < (size_t(1) << 31);
   const unsigned slot = ctx->launch_seq % RT4_OVERLAP_SLOTS;
-  hipStream_t ts = s;  // the trace kernel's stream
-  if (overlap) {
-    const size_t need = npx_all * sizeof(float4);
-    if (ctx->ofcolor_bytes < need) {  // the slots grow to the largest region seen (both idle first)
-      if (ctx->launched) HIP_TRY(hipEventSynchronize(ctx->done));
-      for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) {
-        if (ctx->side[k]) HIP_TRY(hipStreamSynchronize(ctx->side[k]));
-        if (ctx->d_ofcolor[k]) (void)hipFree(ctx->d_ofcolor[k]);
-        ctx->d_ofcolor[k] = nullptr;
-      }
-      ctx->ofcolor_bytes = 0;
-      for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) HIP_TRY(hipMalloc(&ctx->d_ofcolor[k], need));
-      ctx->ofcolor_bytes = need;
-    }
-    a.fcolor = static_cast<float4*>(ctx->d_ofcolor[slot]);
-    a.frame_part[0] = a.part;
-  }
   const Variant& v = variant_for(ctx->shape);
   const bool reuse = (ctx->flags & RT4_FLAG_PRIMARY_REUSE) && ctx->shape != GENERIC;
-  const TraceFn fn = v.trace[ctx->d_wlut ? 1 : 0][reuse ? 1 : 0];
+  const TraceFn fn = trace_fn_of(ctx);
   // grid: what the device holds at once; later blocks would only find the queue empty
-  if (ctx->occ_fn != fn) {
-    int n = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), 256, 0));
-    ctx->occ_fn = fn;
-    ctx->occ_per_cu = n;
+  int per_cu = 0;
+  {
+    const int st = occupancy_of(ctx, fn, &per_cu, err, errlen);
+    if (st != RT4_OK) return st;
   }
-  const int per_cu = ctx->occ_per_cu;
+  const long long items = static_cast<long long>(a.total >> 6);  // tiles of all jobs (and frames)
+  // an overlapped frame with fewer tiles than the chip holds waves runs deep: up to RT4_OVERLAP_SLOTS in flight
+  const bool deep = overlap && overlap_deep(ctx, items, per_cu);
+  if (overlap) {
+    const int st = ensure_overlap_buffer(ctx, deep ? slot : ctx->launch_seq % RT4_OVERLAP_BIG, npx_all * sizeof(float4),
+                                         err, errlen);
+    if (st == kSlotNoMem) overlap = false;  // no memory for the slot buffer: this frame runs serially
+    else if (st != RT4_OK) return st;
+  }
+  hipStream_t ts = s;  // the trace kernel's stream
+  if (overlap) {
+    for (int q = 1; q < n_jobs; q++)
+      a.jobs[q].fc_base = a.jobs[q - 1].fc_base + static_cast<unsigned>(a.jobs[q - 1].reg.w) * static_cast<unsigned>(a.jobs[q - 1].reg.h);
+    a.fcolor = static_cast<float4*>(ctx->d_ofcolor[deep ? slot : ctx->launch_seq % RT4_OVERLAP_BIG]);
+    a.frame_part[0] = a.part;
+  }
   int bpc = per_cu > 0 ? per_cu : 1;
   const unsigned long long frame_work = static_cast<unsigned long long>(a.total) * static_cast<unsigned>(a.samples) *
                                        static_cast<unsigned>(a.reflections_amount + 1);
   if (overlap && frame_work <= RT4_OVERLAP_SHORT_WORK) bpc = bpc > RT4_OVERLAP_GRID_LESS ? bpc - RT4_OVERLAP_GRID_LESS : 1;
   long long blocks = static_cast<long long>(ctx->n_cu) * bpc;
-  const long long items = static_cast<long long>(a.total >> 6);  // tiles of all jobs (and frames)
-  // an overlapped frame with fewer tiles than the chip holds waves runs deep: up to RT4_OVERLAP_SLOTS in flight
-  const bool deep = overlap && items < static_cast<long long>(ctx->n_cu) * (per_cu > 0 ? per_cu : 1) * 4;
   if (overlap) {
     const unsigned sidx = ctx->launch_seq % (deep ? RT4_OVERLAP_SLOTS : RT4_OVERLAP_BIG);
     if (!ctx->side[sidx]) {
@@ -2123,8 +2162,10 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   a.order_ends = nullptr;
   if (reuse) a.eval_counter = ctx->d_eval;
   // The tile order buffer is one per context: a launch on another stream than the previous one
-  // waits for it (launches of one context run in submission order).
-  if (ctx->launched && s != ctx->last_stream) HIP_TRY(hipStreamWaitEvent(ts, ctx->done, 0));
+  // waits for it (launches of one context run in submission order). So does an overlapped launch that
+  // switches between the deep and the big rotation (they share slot buffers 0 .. RT4_OVERLAP_BIG - 1).
+  if (ctx->launched && (s != ctx->last_stream || (overlap && ctx->overlapped && deep != ctx->last_deep)))
+    HIP_TRY(hipStreamWaitEvent(ts, ctx->done, 0));
   // launch s - S is complete before launch s starts: its queue word, frame-colour slot and count slot are
   // free again (launches s - S + 1 .. s - 1 may still be draining: that is the overlap)
   HIP_TRY(hipStreamWaitEvent(ts, ctx->seq_done[slot], 0));
@@ -2182,15 +2223,20 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   unsigned* q = ctx->d_queue + (ctx->launch_seq % QUEUE_SLOTS);
   unsigned* q_next = ctx->d_queue + ((ctx->launch_seq + RT4_OVERLAP_SLOTS) % QUEUE_SLOTS);  // zeroed by this launch
   const unsigned seq = ctx->launch_seq++;
-  if (ctx->queue_dirty && ctx->dirty_seq == seq) {
+  if (ctx->q_dirty[seq % QUEUE_SLOTS]) {
     HIP_TRY(hipMemsetAsync(q, 0, sizeof(unsigned), ts));
-    ctx->queue_dirty = false;
+    ctx->q_dirty[seq % QUEUE_SLOTS] = false;
+  }
+  if (overlap) {
+    ctx->overlapped = true;
+    ctx->last_deep = deep;
   }
   unsigned long long* count = overlap ? ctx->d_ocount + slot : d_counter;
   (void)hipGetLastError();  // a sticky error of an earlier, unrelated call must not be taken for this launch's
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, ts, ctx->d_scene, scene_aux(ctx), a, count,
                      ctx->d_wlut, q, q_next);
   hipError_t le = hipGetLastError();
+  const bool trace_enqueued = le == hipSuccess;
   if (le == hipSuccess && overlap) {
     le = hipEventRecord(ctx->traced[slot], ts);
     if (le == hipSuccess) le = hipStreamWaitEvent(s, ctx->traced[slot], 0);
@@ -2211,8 +2257,13 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   ctx->last_stream = s;
   ctx->launched = true;
   if (le != hipSuccess) {
-    ctx->queue_dirty = true;  // q_next may not be zeroed: launch seq + S does it
-    ctx->dirty_seq = seq + RT4_OVERLAP_SLOTS;
+    ctx->q_dirty[(seq + RT4_OVERLAP_SLOTS) % QUEUE_SLOTS] = true;  // q_next may not be zeroed: its next user does it
+    if (overlap && trace_enqueued) {
+      // the trace runs on the side stream but no fold on the caller's stream covers it: wait for it here (the
+      // scene, the slot buffer and the queue words stay valid), then clear the count it left in its slot
+      (void)hipStreamSynchronize(ts);
+      (void)hipMemsetAsync(count, 0, sizeof(unsigned long long), s);
+    }
     rt4_set_err(err, errlen, "trace kernel launch failed: %s", hipGetErrorString(le));
     return RT4_ERR_HIP;
   }
@@ -2280,6 +2331,32 @@ int rt4_context_reserve_frames(rt4_context* ctx, int32_t w, int32_t h, char* err
   HIP_TRY(hipMemset(ctx->d_fcolor, 0, need));  // first touch here, not in the first pipelined launch
   ctx->fcolor_bytes = need;
   return RT4_OK;
+}
+
+int rt4_context_reserve_overlap(rt4_context* ctx, int32_t w, int32_t h, char* err, size_t errlen) {
+  if (!ctx) return rt4_set_err(err, errlen, "NULL argument"), RT4_ERR_ARG;
+  if (w < 1 || h < 1) return rt4_set_err(err, errlen, "bad size %d x %d", w, h), RT4_ERR_ARG;
+  if (!RT4_OVERLAP_FRAMES || (ctx->flags & RT4_FLAG_SERIAL_FRAMES)) return RT4_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  int per_cu = 0;
+  const int st = occupancy_of(ctx, trace_fn_of(ctx), &per_cu, err, errlen);
+  if (st != RT4_OK) return st;
+  const long long items = static_cast<long long>((w + 7) / 8) * ((h + 7) / 8);
+  const bool deep = overlap_deep(ctx, items, per_cu);
+  const size_t need = static_cast<size_t>(w) * static_cast<size_t>(h) * sizeof(float4);
+  for (int k = 0; k < (deep ? RT4_OVERLAP_SLOTS : RT4_OVERLAP_BIG); k++) {
+    const int r = ensure_overlap_buffer(ctx, static_cast<unsigned>(k), need, err, errlen);
+    if (r == kSlotNoMem) return rt4_set_err(err, errlen, "slot buffer allocation of %zu bytes failed", need), RT4_ERR_HIP;
+    if (r != RT4_OK) return r;
+  }
+  return RT4_OK;
+}
+
+uint64_t rt4_context_overlap_bytes(const rt4_context* ctx) {
+  uint64_t n = 0;
+  if (ctx)
+    for (int k = 0; k < RT4_OVERLAP_SLOTS; k++) n += ctx->ofcolor_cap[k];
+  return n;
 }
 
 int rt4_render_frames_device(rt4_context* ctx, const rt4_uniforms* u, int32_t n_frames, const rt4_region* region,

@@ -77,6 +77,7 @@ FLAG_SAMPLER_LUT = 0x1
 FLAG_GENERIC_KERNEL = 0x2
 FLAG_PRIMARY_REUSE = 0x4
 FLAG_SERIAL_FRAMES = 0x8
+FLAG_OVERLAP_SHALLOW = 0x10  # rt4.h RT4_FLAG_OVERLAP_SHALLOW: at most 3 overlapped launches in flight
 FRAME_RGBA32F, FRAME_RGBA16F, FRAME_RGBA8 = 0, 1, 2
 KEY_FORWARD, KEY_BACK, KEY_RIGHT, KEY_LEFT, KEY_UP, KEY_DOWN, KEY_W_POS, KEY_W_NEG = (1 << i for i in range(8))
 MAX_SECTIONS = 3
@@ -205,6 +206,8 @@ def _load(path=None):
         "rt4_bands_unpermute_device": ([c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                         c_void_p] + E, c_int),
         "rt4_context_frame_scratch_bytes": ([c_void_p], c_uint64),
+        "rt4_context_overlap_bytes": ([c_void_p], c_uint64),
+        "rt4_context_reserve_overlap": ([c_void_p, c_int32, c_int32] + E, c_int),
         "rt4_accum_save": ([c_char_p, c_void_p, c_int32, c_int32, c_int32, c_int64, c_int64, c_uint32] + E, c_int),
         "rt4_accum_info": ([c_char_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32), POINTER(c_int64),
                             POINTER(c_uint32)] + E, c_int),
@@ -242,7 +245,7 @@ EXPORTED = (
     "rt4_camera_init rt4_camera_rotate rt4_camera_mouse_move rt4_camera_wheel rt4_camera_move "
     "rt4_camera_frame_uniforms rt4_write_ppm rt4_frame_format_bytes rt4_render_device_ex rt4_render_host_ex rt4_progressive_uniforms rt4_render_sections_device "
     "rt4_debug_verify_div rt4_debug_sky_threshold rt4_context_evaluated rt4_render_frames_device rt4_context_reserve_frames rt4_context_frames_per_launch "
-    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_accum_save rt4_accum_info rt4_accum_load rt4_write_png "
+    "rt4_band_plan rt4_bands_unpermute_device rt4_context_frame_scratch_bytes rt4_context_overlap_bytes rt4_context_reserve_overlap rt4_accum_save rt4_accum_info rt4_accum_load rt4_write_png "
     "rt4_accum_save_key rt4_accum_key rt4_accum_key_of"
 ).split()
 
@@ -625,6 +628,15 @@ class Tracer:
     def frame_scratch_bytes(self) -> int:
         """Bytes of the context's frame-colour scratch (0: none allocated)."""
         return int(self._lib.rt4_context_frame_scratch_bytes(self._h))
+
+    def overlap_bytes(self) -> int:
+        """Bytes of the context's overlap slot buffers (rt4.h rt4_context_overlap_bytes)."""
+        return int(self._lib.rt4_context_overlap_bytes(self._h))
+
+    def reserve_overlap(self, w: int, h: int) -> None:
+        """Allocate the slot buffers overlapped single-frame launches of a w x h image use, up front."""
+        err = _errbuf()
+        _check(self._lib.rt4_context_reserve_overlap(self._h, w, h, err, len(err)), err)
 
     def render_sections_device(self, jobs, fmt: int = FRAME_RGBA32F, counter_ptr: int = 0, stream: int = 0) -> None:
         """One launch over up to three images: jobs = [(uniforms, region, frame_ptr, row_stride_px), ...]."""

@@ -12,6 +12,7 @@ bit-identical to a 1-GPU render.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 
@@ -127,7 +128,88 @@ def gather_frame(local, plan: BandPlan, rank: int, group=None):
         if recv is None:
             recv = _RECV_CACHE[key] = torch.empty((plan.world,) + tuple(local.shape), dtype=local.dtype,
                                                   device=local.device)
+    fail = os.environ.get("RT4_GATHER_FAIL_RANK")  # test hook: this rank's part of the gather fails
+    if fail is not None and int(fail) == rank:
+        raise GatherError(f"gather failure injected (RT4_GATHER_FAIL_RANK={rank})")
     dist.gather(local, gather_list=list(recv.unbind(0)) if recv is not None else None, dst=0, group=group)
     if rank != 0:
         return None
     return unpermute(recv, plan)
+
+
+# ---- failure handling of the gather ------------------------------------------------------
+# A rank whose part of a collective fails leaves its peers waiting inside theirs (RCCL: their gather kernels wait
+# for its data; gloo: their receives). The failing rank posts its error to the process group's key-value store
+# and exits; a peer learns of it either from its own collective failing (gloo sees the closed connection) or, on
+# RCCL, while it waits for its stream with wait_or_failure, which polls the store instead of blocking, and then
+# exits too. Every rank ends with status 1 and a message naming the failed rank, none hangs.
+FAIL_KEY = "rt4/gather_failed"
+
+
+class GatherError(RuntimeError):
+    pass
+
+
+def _store():
+    try:
+        import torch.distributed.distributed_c10d as c10d
+
+        return c10d._get_default_store()
+    except Exception:  # no process group, or a launcher without a store
+        return None
+
+
+def report_failure(rank: int, msg: str) -> None:
+    """Posts `rank: msg` to the store (the first report is kept)."""
+    st = _store()
+    if st is not None:
+        try:
+            st.compare_set(FAIL_KEY, "", f"rank {rank}: {msg}")
+        except Exception:
+            pass
+
+
+def failure() -> str | None:
+    """The failure a rank reported, or None."""
+    st = _store()
+    try:
+        if st is not None and st.check([FAIL_KEY]):
+            return st.get(FAIL_KEY).decode()
+    except Exception:
+        pass
+    return None
+
+
+def wait_or_failure(stream=None, check_s: float = 0.01) -> str | None:
+    """Waits on the host for the work enqueued so far on `stream` (the gathers included), checking the store every
+    check_s: None when the work completed, a failed rank's report when one arrived first (that rank's collective
+    will never complete). The completion itself is polled without sleeping, so a timed region that ends with this
+    wait ends within microseconds of the device work (the store's round trips only every check_s)."""
+    import time
+
+    import torch
+
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    next_check = time.perf_counter() + check_s
+    while not ev.query():
+        now = time.perf_counter()
+        if now >= next_check:
+            f = failure()
+            if f is not None:
+                return f
+            next_check = now + check_s
+    return None
+
+
+def exit_failed(rank: int, msg: str, log=None) -> None:
+    """Reports this rank's failure (or the one another rank reported first) and ends the process with status 1
+    without waiting for collectives that will never complete (os._exit: no interpreter shutdown, which would
+    join the process group's pending work)."""
+    import sys
+
+    report_failure(rank, msg)
+    first = failure() or f"rank {rank}: {msg}"
+    text = f"rank {rank}: stopping, the gather failed: {first}"
+    (log or (lambda t: print(t, file=sys.stderr, flush=True)))(text)
+    os._exit(1)

@@ -432,10 +432,23 @@ def main():
         tracer.render_frames_device([uniforms() for _ in range(n)], reg, frame.data_ptr(), fmt, plan.width, cnt_ptr, sptr)
 
     def gather_once():
-        if rehearse:
-            shard.gather_frame(frame.cpu(), plan, rank)
-        else:
-            shard.gather_frame(frame, plan, rank)  # the frame assembled (un-permuted) on rank 0
+        # a rank whose part of the gather fails posts the error and exits; its peers exit when their own gather
+        # fails (gloo) or when sync() finds the report (RCCL): status 1 naming the rank, no hang (shard.py)
+        try:
+            if rehearse:
+                shard.gather_frame(frame.cpu(), plan, rank)
+            else:
+                shard.gather_frame(frame, plan, rank)  # the frame assembled (un-permuted) on rank 0
+        except Exception as e:  # noqa: BLE001 - any failure of the collective ends every rank
+            shard.exit_failed(rank, f"{type(e).__name__}: {e}")
+
+    def sync():
+        # torch.cuda.synchronize, but with N > 1 a wait that also watches for a failed peer's report
+        if world > 1:
+            f = shard.wait_or_failure(stream)
+            if f is not None:
+                shard.exit_failed(rank, "a peer's gather failed")
+        torch.cuda.synchronize()
 
     def gather():
         g0 = torch.cuda.Event(enable_timing=True)
@@ -458,7 +471,7 @@ def main():
         # one gather outside the timed region: the collective's one-time set-up (RCCL's point-to-point
         # connections behind dist.gather, the receive buffers' first allocation) is not part of a frame
         gather_once()
-    torch.cuda.synchronize()
+    sync()
     counter.zero_()
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -479,7 +492,7 @@ def main():
                 gather()
     if world > 1 and args.gather == "final":
         gather()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -523,7 +536,10 @@ def main():
                      "iteration; same frames, same image and count as the pipelined headline",
             "value": n_f / el_f, "unit": "ray-bounce intersections/s",
             "ms_per_step": el_f / args.steps * 1e3,
-            "kernel_ms": f_start[0].elapsed_time(f_end[-1]) / args.steps,  # first start to last end (overlap)
+            # first start to last end on the caller's stream (the traces overlap): a device span per frame, which
+            # includes host submission gaps between launches, not a kernel-only time
+            "kernel_ms": f_start[0].elapsed_time(f_end[-1]) / args.steps,
+            "kernel_ms_kind": "device span per frame: first start event to last end event on the caller's stream",
             "intersections_per_step": n_f / args.steps,
         }
 
@@ -624,6 +640,9 @@ def main():
             "intersections_per_step": n_total / args.steps,
             "nominal_bound_per_step": plan.width * plan.height * args.spp * (args.bounces + 1),
             "kernel_ms": kernel_ms,
+            "kernel_ms_kind": ("HIP events around the pipelined launch(es) and the fold on the launch stream, per frame"
+                               if pipelined else "device span per frame: first start event to last end event on the "
+                               "caller's stream (the overlapped traces run on side streams)"),
             "frames_per_launch": fpl,
             "setup_ms": setup,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),

@@ -335,13 +335,27 @@ typedef struct rt4_context rt4_context;
  * actually evaluated. Specialised kernels only (ignored with RT4_FLAG_GENERIC_KERNEL or a generic
  * scene). SURVEY.md 8(d): a rate measured with it is labelled reference-equivalent. */
 #define RT4_FLAG_PRIMARY_REUSE 0x4u
-/* Single-frame launches (rt4_render_device[_ex], one-section rt4_render_sections_device) run entirely on
- * the caller's stream. By default their trace kernel runs on one of two context-owned side streams and
- * writes the frame's light sums to a slot buffer, and only the blend into the frame (and the count) runs on
- * the caller's stream: back-to-back frames (a moving camera, main.cpp:93) then overlap each frame's trace with
- * the previous frame's drain. Stream semantics are unchanged: the frame and the counter are written in the
- * caller's stream order. Images are identical either way. */
+/* Overlapped launches (the default). A single-frame launch (rt4_render_device[_ex],
+ * rt4_render_sections_device) runs its trace kernel on a context-owned side stream and writes the frame's light
+ * sums to a context-owned slot buffer; only the blend into the frame (and the count) runs on the caller's stream.
+ * Back-to-back frames (a moving camera, main.cpp:93; the 4D view's three sections, three_window_group.cpp:42-46)
+ * then overlap each frame's trace with the previous frames' drain. Stream semantics are unchanged: the frame and
+ * the counter are written in the caller's stream order; images and counts are identical to serial launches.
+ * Depth and memory: a launch with fewer 8x8 tiles than the chip holds waves (~7000 tiles: the 4D view's sections
+ * at properties.txt sizes) keeps up to 8 launches in flight on 8 side streams with 8 slot buffers; any larger one
+ * up to 3, with 3 buffers. A slot buffer is 16 B per pixel of the largest launch it served: a 1080p frame uses
+ * 3 x 33 MB, a 4K frame 3 x 133 MB, small frames at most 8 x 7.3 MB (rt4_context_overlap_bytes). The first launch
+ * that needs a larger buffer waits on the host for the launches in flight and allocates it
+ * (rt4_context_reserve_overlap does that ahead of time); if the allocation fails, that frame runs serially.
+ * Hardware queues: the 8 side streams of the deep overlap share HIP's default four hardware queues per process;
+ * set GPU_MAX_HW_QUEUES=8 in the environment before the process first touches HIP to give each its own (the 4D
+ * view loop on config 2's scene: 0.25 ms per frame with the default, 0.17 ms with 8; frames that fill the chip
+ * are unaffected). */
+/* Every launch runs entirely on the caller's stream (no side streams, no slot buffers). */
 #define RT4_FLAG_SERIAL_FRAMES 0x8u
+/* Caps the overlap at 3 launches in flight for every frame size (3 side streams, 3 slot buffers): for processes
+ * that keep HIP's four hardware queues or want the smaller footprint. Images and counts are unchanged. */
+#define RT4_FLAG_OVERLAP_SHALLOW 0x10u
 
 int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err, size_t errlen);
 /* Uploads a scene (the reference recompiles the shader: src/main.cpp:25-39). Waits for the
@@ -366,9 +380,11 @@ typedef struct rt4_region {
  * Holds old_frame on entry and mix(old, new, part) on return (shader.frag:524-527).
  * d_counter (may be NULL): device uint64 incremented by the number of find_intersection calls
  * (one per ray-bounce, shader.frag:475). stream: hipStream_t (NULL = default stream).
- * Asynchronous: no host synchronisation and no allocation for launches of up to 2^18 8x8 tiles
- * (16.7 M pixels; a larger one grows the context's tile-order buffer once). Launches of one context
- * run in submission order: a launch on another stream than the previous one waits for it. */
+ * Asynchronous: no host synchronisation and no allocation once the context's buffers hold the launch: the
+ * tile-order buffer covers 2^18 8x8 tiles (16.7 M pixels; a larger launch grows it once) and the overlap's slot
+ * buffers grow to the largest frame seen (RT4_FLAG_SERIAL_FRAMES: the first launch of a larger frame waits for
+ * the launches in flight and allocates; rt4_context_reserve_overlap does it ahead of time). Launches of one
+ * context run in submission order: a launch on another stream than the previous one waits for it. */
 int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
                       int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err,
                       size_t errlen);
@@ -470,6 +486,14 @@ int rt4_bands_unpermute_device(const void* d_gathered, void* d_image, int32_t wi
 /* Bytes of the context's frame-colour scratch for pipelined frames (0 before any pipelined launch or
  * reservation; a scene that runs frame by frame never allocates it). */
 uint64_t rt4_context_frame_scratch_bytes(const rt4_context* ctx);
+/* Bytes of the context's overlap slot buffers (RT4_FLAG_SERIAL_FRAMES: 0 before any single-frame launch). */
+uint64_t rt4_context_overlap_bytes(const rt4_context* ctx);
+/* Allocates the slot buffers that overlapped single-frame launches of one w x h image use with the context's
+ * current scene (3, or 8 for a frame too small to fill the chip), so that the first such launch neither
+ * allocates nor synchronises. Waits for the context's launches in flight when it grows a buffer. A no-op for a
+ * context made with RT4_FLAG_SERIAL_FRAMES. For the 4D view's sections pass w x h with w * h >= the sections'
+ * pixels together. */
+int rt4_context_reserve_overlap(rt4_context* ctx, int32_t w, int32_t h, char* err, size_t errlen);
 enum rt4_eval_fn {
   RT4_EVAL_ACOS = 0, RT4_EVAL_ASIN = 1, RT4_EVAL_SIN = 2, RT4_EVAL_COS = 3,
   RT4_EVAL_VOLUME_BY_W = 4, /* shader.frag:136-138 */

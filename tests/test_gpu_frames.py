@@ -504,3 +504,69 @@ def test_overlapped_sections_equal_serial(rt4, name, fmt):
         for q in range(4):
             eq = bits_equal(a[q], b[q])
             assert eq.all(), f"frame {n} image {q}: {(~eq).sum()} values differ"
+
+
+@pytest.mark.parametrize("name", ["sphere", "all_primitives"])
+def test_overlap_rotations_cap_and_memory(rt4, name):
+    """The overlap's two rotations (rt4.h RT4_FLAG_SERIAL_FRAMES / RT4_FLAG_OVERLAP_SHALLOW; DESIGN.md §4.28,
+    ADVICE r04): small frames run 8 deep with 8 slot buffers, frames that fill the chip 3 deep with 3 buffers, and
+    switching between them drains the launches in flight. Small, big and small frames again, with the default, the
+    3-deep cap and serial launches: every frame and the count equal the serial ones bit for bit, and the slot memory
+    is what rt4.h states: launch s uses buffer s % 8 when small, s % 3 when big (so launches 0-2 and 6-7 leave small
+    buffers 6 and 7 and big buffers 0-2 by default), buffer s % 3 with the cap, none serial."""
+    import torch
+
+    small, big = (131, 77), (1024, 640)  # 170 tiles; 10240 tiles: more than the chip holds waves
+    seq = [small] * 3 + [big] * 3 + [small] * 2
+    us = [rt4.make_uniforms(w, h, samples=2, reflections=2, seed=300 + n, fi=3.0 * n) for n, (w, h) in enumerate(seq)]
+    px = {s: s[0] * s[1] * 16 for s in (small, big)}
+    expect_bytes = {rt4.FLAG_SAMPLER_LUT: 3 * px[big] + 2 * px[small],
+                    rt4.FLAG_SAMPLER_LUT | rt4.FLAG_OVERLAP_SHALLOW: 3 * px[big],
+                    rt4.FLAG_SAMPLER_LUT | rt4.FLAG_SERIAL_FRAMES: 0}
+    runs = {}
+    for flags, want in expect_bytes.items():
+        t = rt4.Tracer(device=0, flags=flags, scene=rt4.Scene.named(name))
+        try:
+            frs = {s: torch.zeros((s[1], s[0], 4), device="cuda") for s in (small, big)}
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            stream = torch.cuda.current_stream().cuda_stream
+            out = []
+            for (w, h), u in zip(seq, us):
+                t.render_device(u, rt4.region(w, h), frs[(w, h)].data_ptr(), w, cnt.data_ptr(), stream)
+                out.append(frs[(w, h)].clone())
+            torch.cuda.synchronize()
+            assert t.overlap_bytes() == want, (flags, t.overlap_bytes(), want)
+        finally:
+            t.close()
+        runs[flags] = ([x.cpu().numpy() for x in out], int(cnt.item()))
+    ref_frames, ref_count = runs[rt4.FLAG_SAMPLER_LUT | rt4.FLAG_SERIAL_FRAMES]
+    for flags, (frames, count) in runs.items():
+        assert count == ref_count, (flags, count, ref_count)
+        for n, (a, b) in enumerate(zip(frames, ref_frames)):
+            eq = bits_equal(a, b)
+            assert eq.all(), f"flags {flags:#x} frame {n}: {(~eq).sum()} values differ"
+
+
+def test_reserve_overlap_allocates_ahead(rt4):
+    """rt4_context_reserve_overlap sizes the slot buffers a frame of that size uses (3 for a frame that fills
+    the chip), so its first launch grows nothing; a serial context reserves nothing."""
+    import torch
+
+    W, H = 1024, 640
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT, scene=rt4.Scene.named("sphere"))
+    try:
+        assert t.overlap_bytes() == 0
+        t.reserve_overlap(W, H)
+        assert t.overlap_bytes() == 3 * W * H * 16
+        fr = torch.zeros((H, W, 4), device="cuda")
+        t.render_device(rt4.make_uniforms(W, H, samples=1, reflections=1, seed=5), rt4.region(W, H), fr.data_ptr(), W)
+        torch.cuda.synchronize()
+        assert t.overlap_bytes() == 3 * W * H * 16
+    finally:
+        t.close()
+    t = rt4.Tracer(device=0, flags=rt4.FLAG_SAMPLER_LUT | rt4.FLAG_SERIAL_FRAMES, scene=rt4.Scene.named("sphere"))
+    try:
+        t.reserve_overlap(W, H)
+        assert t.overlap_bytes() == 0
+    finally:
+        t.close()

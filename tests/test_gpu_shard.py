@@ -215,6 +215,23 @@ def test_cpp_host_bands_failed_rank_skips_the_collective(rt4, tmp_path, gpus, re
     assert not os.path.exists(pre + "_yxz.ppm")
 
 
+@pytest.mark.parametrize("gpus,rehearse,fail", [(3, True, 1), (8, True, 7), (1, False, 0)])
+def test_cpp_host_bands_failed_gather_aborts_cleanly(rt4, tmp_path, gpus, rehearse, fail):
+    """A rank whose part of the gather fails (RT4_RENDER_FAIL_STAGE=gather: it does not enqueue its ncclGather,
+    as when the call returns an error): the ranks agree after the gather was enqueued, every
+    rank aborts its communicator (ncclCommAbort; one-rank RCCL communicator on this box) instead of waiting for the
+    peer, and the program exits with status 1 naming the rank, without hanging and without an image."""
+    import os
+
+    pre = str(tmp_path / "g")
+    r = _run_render(rt4, ["-p", _props_with(tmp_path, 2, 2), "-s", "sphere", "-n", "3", "-W", "160", "-H", "90",
+                          "--gpus", str(gpus), "-o", pre] + (["--rehearse"] if rehearse else []),
+                    env={"RT4_RENDER_FAIL_RANK": str(fail), "RT4_RENDER_FAIL_STAGE": "gather"})
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert f"rank {fail}: " in r.stderr and "failure injected (RT4_RENDER_FAIL_STAGE=gather)" in r.stderr, r.stderr
+    assert not os.path.exists(pre + "_yxz.ppm")
+
+
 def test_reserve_frames_sizes_one_chunk(rt4):
     """rt4_context_reserve_frames allocates nothing for a region that runs frame by frame (wider than the
     pipelined pixel word holds), and exactly one chunk of frames otherwise: config 4's 4K

@@ -165,3 +165,55 @@ def test_cpp_host_bands_error_path_exits_cleanly(rt4, tmp_path):
     assert r.returncode == 1, r.stdout + r.stderr
     assert "rank 1" in r.stderr, r.stderr
     assert not os.path.exists(pre + "_yxz.ppm")
+
+
+def _gather_fail_worker(rank, world, port, out_dir):
+    os.environ["RT4_GATHER_FAIL_RANK"] = "1"
+    sys.path.insert(0, ROOT)
+    # the store lives in the test process, as torchrun's agent hosts it for bench.py's ranks
+    store = dist.TCPStore("127.0.0.1", port, world, is_master=False)
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
+    shard = importlib.import_module("4d_ray_tracing_amd.shard")
+    plan = shard.make_plan(16, height=40, world=world, band=8)
+    local = torch.zeros((plan.rows_max, plan.width, 4))
+
+    def log(text):
+        with open(os.path.join(out_dir, f"rank{rank}.log"), "w") as f:
+            f.write(text)
+
+    try:  # bench.py's gather_once: any failure of the collective ends the rank via shard.exit_failed
+        shard.gather_frame(local, plan, rank)
+    except Exception as e:  # noqa: BLE001
+        shard.exit_failed(rank, f"{type(e).__name__}: {e}", log=log)
+    try:  # a non-root rank's gather may complete (its send is done); its next collective then fails
+        dist.barrier()
+    except Exception as e:  # noqa: BLE001
+        shard.exit_failed(rank, f"{type(e).__name__}: {e}", log=log)
+    log("gather returned")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_failure_on_one_rank_ends_every_rank(tmp_path, world):
+    """VERDICT r04 item 5 (bench.py's gather, shard.gather_frame): rank 1's part of the gather fails
+    (RT4_GATHER_FAIL_RANK). It posts the error to the process group's store and exits; the other ranks fail in
+    their gather (the root, waiting for rank 1's shard) or in their next collective (a rank whose send completed)
+    when its connection closes (gloo), and exit too. Every rank ends with status 1 and names rank 1; none hangs."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    store = dist.TCPStore("127.0.0.1", port, world, is_master=True, wait_for_workers=False)  # noqa: F841
+    procs = [ctx.Process(target=_gather_fail_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "a rank hung after the gather failure"
+    assert [p.exitcode for p in procs] == [1] * world
+    for r in range(world):
+        text = (tmp_path / f"rank{r}.log").read_text()
+        assert "rank 1: GatherError: gather failure injected" in text, (r, text)
