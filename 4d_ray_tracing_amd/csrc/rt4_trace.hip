@@ -120,6 +120,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
+#ifndef RT4_LSUM_REG_TIGER
+#define RT4_LSUM_REG_TIGER 1  // the light sum in VGPRs in the tiger kernels too (r05, at their 5-wave bound: config 4 +1 %, config 5 +-0)
+#endif
 #if defined(RT4_STAMPS) || defined(RT4_LANESTATS) || defined(RT4_TAILSTATS)
 #define RT4_OVERLAP_FRAMES 0  // the diagnostic builds write counter[1..]: the caller's buffer, never a count slot
 #endif
@@ -575,7 +578,8 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
   // (not in the deferred-sphere kernel since r04: its light sum in LDS and the exact tests recomputing the
   // cull's dots (DEFER_GEO) bring it to 72 VGPRs, 7 waves/SIMD with no spill in the loop: config 2 +3-4 %,
   // profiles/r04_ab.txt)
-  constexpr bool LSUM_REG = RT4_LSUM_REG && K != GENERIC && !(K & (K_TIGER | K_HYPERCUBE)) && !(DEFER && !RT4_DEFER_GEO);
+  constexpr bool LSUM_REG = (RT4_LSUM_REG && K != GENERIC && !(K & (K_TIGER | K_HYPERCUBE)) && !(DEFER && !RT4_DEFER_GEO)) ||
+                            (RT4_LSUM_REG_TIGER && K != GENERIC && (K & K_TIGER) && !REUSE);
   float4 lsum_reg = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   auto lsum_load = [&]() -> float4 {
     if constexpr (LSUM_REG) return lsum_reg;
