@@ -120,8 +120,14 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_LSUM_REG
 #define RT4_LSUM_REG 1
 #endif
+#ifndef RT4_FLUSH_REMAT
+#define RT4_FLUSH_REMAT 1  // the outbox path recomputes the lane / wave / sample count where it runs (r05)
+#endif
+#ifndef RT4_WAVE_COUNT
+#define RT4_WAVE_COUNT 1  // intersection counts in a scalar register per wave (kernels without primary reuse)
+#endif
 #ifndef RT4_LSUM_REG_TIGER
-#define RT4_LSUM_REG_TIGER 1  // the light sum in VGPRs in the tiger kernels too (r05, at their 5-wave bound: config 4 +1 %, config 5 +-0)
+#define RT4_LSUM_REG_TIGER 1  // the light sum in VGPRs in the tiger kernels bounded to 5 waves (r05: config 4 +1 % at 5)
 #endif
 #if defined(RT4_STAMPS) || defined(RT4_LANESTATS) || defined(RT4_TAILSTATS)
 #define RT4_OVERLAP_FRAMES 0  // the diagnostic builds write counter[1..]: the caller's buffer, never a count slot
@@ -167,10 +173,16 @@ static_assert(RT4_OVERLAP_BIG >= 2 && RT4_OVERLAP_BIG <= RT4_OVERLAP_SLOTS, "ove
 // Which build hit it depended on scheduling: the -amdgpu-sched-strategy=iterative-ilp build and a build with the
 // sphere cull's && / || written as & / | computed other images and counts; the shipped one did not, by luck.
 #ifndef RT4_WAVES_MIRROR
-#define RT4_WAVES_MIRROR 5  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
+#define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
+#endif
+#ifndef RT4_WAVES_MIRROR_REUSE
+#define RT4_WAVES_MIRROR_REUSE 5  // its primary-reuse instantiations (spilled in the loop at 6)
 #endif
 #ifndef RT4_WAVES_ALLPRIM
-#define RT4_WAVES_ALLPRIM 5  // tiger kernels with other groups (all_primitives: BASELINE config 5)
+#define RT4_WAVES_ALLPRIM 6  // tiger kernels with other groups (all_primitives: BASELINE config 5), sampler table
+#endif
+#ifndef RT4_WAVES_ALLPRIM_INLINE
+#define RT4_WAVES_ALLPRIM_INLINE 5  // the same with the inline Newton sampler (spilled in the loop at 6)
 #endif
 #ifndef RT4_WAVES_ALLPRIM_REUSE
 #define RT4_WAVES_ALLPRIM_REUSE 4  // their primary-reuse instantiations (96 VGPRs at 5 still spilled)
@@ -296,6 +308,14 @@ __device__ __forceinline__ V3 final_light(const rt4_scene_desc* __restrict__ S, 
   return sky;
 }
 
+// The lane's index in its wave from mbcnt, evaluated where it stands (asm volatile: not merged with another
+// evaluation, so no register carries it across the loop body; RT4_FLUSH_REMAT)
+__device__ __forceinline__ unsigned rt4_lane_id() {
+  unsigned l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 struct RngState {
   uint32_t base;  // bits(scr.x) ^ (bits(scr.y) << 9) ^ uint_seed   (shader.frag:106-107)
   uint32_t iter;  // rand_iter_seed                                (shader.frag:92, :105)
@@ -396,8 +416,13 @@ __device__ __forceinline__ Cand unpack_cand(float4 v) {
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 
 // light /= samples; light_to_color (shader.frag:522-526)
+template <bool REMAT = false>
 __device__ __forceinline__ V3 tone_map(const KernelArgs& a, V3 light) {
-  const float ns = static_cast<float>(a.samples);
+  int samples = a.samples;
+  // converted where it is used: a conversion hoisted out of the trace loop holds a VGPR across it for the once-per-
+  // pixel write (spilled in the register-bound kernels; RT4_FLUSH_REMAT)
+  if (REMAT) asm volatile("" : "+s"(samples));
+  const float ns = static_cast<float>(samples);
   light = V3{light.x / ns, light.y / ns, light.z / ns};
   const float k = a.k;
   return V3{1.0f - 1.0f / sfma_(k, light.x, 1.0f), 1.0f - 1.0f / sfma_(k, light.y, 1.0f),
@@ -439,9 +464,10 @@ __device__ __forceinline__ uint32_t blend_u8(V3 c, float part, uint32_t o) {
 }
 
 // The pixel's light sum, tone-mapped and blended into the launch's frame (shader.frag:522-527).
+template <bool REMAT>
 __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& J, int pk, V3 light) {
   const int j = pk & 0xFFFF, i = (pk >> 16) & 0x3FFF;
-  const V3 c = tone_map(a, light);
+  const V3 c = tone_map<REMAT>(a, light);
   const float part = a.part;
   char* base = static_cast<char*>(J.frame);
   const int64_t at = static_cast<int64_t>(i) * J.row_stride_px + j;
@@ -463,7 +489,7 @@ __device__ __forceinline__ void write_pixel(const KernelArgs& a, const JobArgs& 
 // specialised for three or more spaces (the mirror room of
 // config 4) at 6 (+2.3 %); the one-space tiger kernel and everything else keep the allocator's choice
 // (a 6-wave bound costs the one-space tiger 1.2 %).
-constexpr int min_waves_of(uint32_t K, bool reuse = false) {
+constexpr int min_waves_of(uint32_t K, bool reuse = false, bool lut = true) {
   if (K == GENERIC) return RT4_WAVES_PER_SIMD;
   if (!(K & K_TIGER)) {
     if ((K >> 8) == 0) return RT4_WAVES_PER_SIMD;  // runtime counts
@@ -475,8 +501,12 @@ constexpr int min_waves_of(uint32_t K, bool reuse = false) {
     if (reuse && (K & K_UNION)) return RT4_WAVES_UNION_REUSE;
     return reuse ? 6 : RT4_WAVES_EXACT;  // exact-count shapes (SH() fields)
   }
-  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE)) return reuse ? RT4_WAVES_ALLPRIM_REUSE : RT4_WAVES_ALLPRIM;
-  return ((K >> 8) & 0xFFu) >= 4 ? RT4_WAVES_MIRROR : RT4_WAVES_PER_SIMD;  // SH(): space count + 1 in bits 8..15
+  // the tiger kernels: the bound at which each instantiation runs its trace loop without scratch
+  if ((K >> 8) == 0) return RT4_WAVES_PER_SIMD;  // runtime counts: the allocator's choice (no spill)
+  if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE))
+    return reuse ? RT4_WAVES_ALLPRIM_REUSE : (lut ? RT4_WAVES_ALLPRIM : RT4_WAVES_ALLPRIM_INLINE);
+  if (((K >> 8) & 0xFFu) >= 4) return reuse ? RT4_WAVES_MIRROR_REUSE : RT4_WAVES_MIRROR;  // SH(): space count + 1, bits 8..15
+  return RT4_WAVES_PER_SIMD;
 }
 
 // Phase-aligned refill for this kernel (RT4_PHASE_REFILL): scenes with a tiger or >= 3 spaces (closed rooms).
@@ -488,7 +518,7 @@ constexpr bool phase_refill_of(uint32_t K) {
 }
 
 template <uint32_t K, bool LUT, bool REUSE>
-__global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
+__global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_kernel(const rt4_scene_desc* __restrict__ S,
                                                         const SceneAux* __restrict__ X, const KernelArgs a,
                                                         unsigned long long* __restrict__ counter,
                                                         const WEntry* __restrict__ wlut, unsigned* __restrict__ queue,
@@ -579,7 +609,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
   // cull's dots (DEFER_GEO) bring it to 72 VGPRs, 7 waves/SIMD with no spill in the loop: config 2 +3-4 %,
   // profiles/r04_ab.txt)
   constexpr bool LSUM_REG = (RT4_LSUM_REG && K != GENERIC && !(K & (K_TIGER | K_HYPERCUBE)) && !(DEFER && !RT4_DEFER_GEO)) ||
-                            (RT4_LSUM_REG_TIGER && K != GENERIC && (K & K_TIGER) && !REUSE);
+                            (RT4_LSUM_REG_TIGER && K != GENERIC && (K & K_TIGER) && !REUSE && min_waves_of(K, REUSE, LUT) <= 5);
   float4 lsum_reg = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   auto lsum_load = [&]() -> float4 {
     if constexpr (LSUM_REG) return lsum_reg;
@@ -601,6 +631,12 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
   __shared__ uint2 lds_in_px[256];
   __shared__ float4 lds_out[256];
   const unsigned wbase = threadIdx.x & ~63u;
+  // RT4_FLUSH_REMAT (the tiger kernels): the outbox (retire, flush_ring: once per finished pixel / per 64) takes the
+  // wave's first thread from a scalar register and the lane from mbcnt where it runs, so no VGPR keeps them (or their
+  // LDS addresses) live across the tiger test, the loop's register peak; there they were spilled. The sphere and
+  // hypercube kernels measured 1.4 % / 5.7 % slower with it (profiles/r05_ab.txt) and keep the plain form.
+  constexpr bool REMAT = RT4_FLUSH_REMAT && K != GENERIC && (K & K_TIGER);
+  const unsigned wave_s = __builtin_amdgcn_readfirstlane(wbase);
   unsigned in_next = 64;  // wave-uniform: next inbox entry to hand out (64: empty)
   // RT4_CLAIM_TILES > 1: one atomic claims that many consecutive tiles; the spare ones are used in turn.
   // A spare position past the end of the queue reports it exhausted like a fresh claim.
@@ -614,7 +650,12 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
   uint32_t in_seed = useed;  // wave-uniform: the seed of the inbox's frame
   unsigned ring_n = 0;    // wave-uniform: outbox entries waiting to be written
   int s = 0, b = 0;
-  uint32_t n_inter = 0, n_eval = 0;  // find_intersection calls of the reference / evaluated here
+  uint32_t n_inter = 0, n_eval = 0;  // find_intersection calls of the reference / evaluated here (per lane, REUSE)
+  // Without primary reuse every counted call is evaluated and a lane adds at most one per iteration: the wave
+  // counts them in a wave-uniform (scalar) register from one ballot per iteration instead of a VGPR per lane,
+  // which frees a register in the register-bound tiger kernels (RT4_WAVE_COUNT).
+  constexpr bool WAVE_COUNT = RT4_WAVE_COUNT && !REUSE && K != GENERIC && (K & K_TIGER);
+  unsigned long long w_inter = 0;
 
 #ifdef RT4_LANESTATS
   unsigned long long ls[20] = {};
@@ -631,8 +672,9 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
   // Writes the outbox ring (lane q takes entry q); one wave-uniform pass per job, so every job's frame
   // pointer and stride stay scalar.
   auto flush_ring = [&]() {
-    if (lane < ring_n) {
-      const float4 lp = lds_out[wbase + lane];
+    const unsigned fl = REMAT ? rt4_lane_id() : lane;
+    if (fl < ring_n) {
+      const float4 lp = lds_out[(REMAT ? wave_s : wbase) + fl];
       const int pk = __float_as_int(lp.w);
 #ifdef RT4_GUARD_WRITES  // diagnostic builds only (tools/variant_probe.py): drop a pixel word outside the launch
       const unsigned gj = a.fcolor ? pk & 0x1FFF : pk & 0xFFFF, gi = a.fcolor ? (pk >> 13) & 0x1FFF : (pk >> 16) & 0x3FFF;
@@ -655,7 +697,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
         }
       } else {
         for (int jb = 0; jb < a.n_jobs; jb++)
-          if (((pk >> 30) & 3) == jb) write_pixel(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
+          if (((pk >> 30) & 3) == jb) write_pixel<REMAT>(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
       }
     }
     ring_n = 0;
@@ -670,7 +712,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
       if (pending) {
         const unsigned r = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(pm >> 32),
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(pm), 0u));
-        lds_out[wbase + ring_n + r] = lsum_load();
+        lds_out[(REMAT ? wave_s : wbase) + ring_n + r] = lsum_load();
         pending = false;
       }
       ring_n += np;
@@ -1003,10 +1045,13 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
     }
     bool end_early = false, end_full = false;  // CLOCK: the lane's sample ended before / at the bounce limit
     if (active && parked) RT4_LS(9);  // lanes waiting (deferred exact tests, or held for the wave clock)
+    if constexpr (WAVE_COUNT) w_inter += static_cast<unsigned long long>(__popcll(__ballot(active && !parked)));
     if (active && !parked) {
       RT4_LS(1);
-      ++n_inter;
-      if (!cached) ++n_eval;
+      if constexpr (!WAVE_COUNT) {
+        ++n_inter;
+        if (!cached) ++n_eval;
+      }
       if constexpr (REUSE) {
         if (s == 0 && b == 0) cold[512] = pack_cand(c);  // the pixel's primary candidate
       }
@@ -1110,13 +1155,19 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE)) void rt4_trace_kernel(
   }
 #endif
   if (counter) {  // wave-level sum, one atomic per wave
-    unsigned long long v = n_inter;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    unsigned long long v = w_inter;
+    if constexpr (!WAVE_COUNT) {
+      v = n_inter;
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    }
     if (lane == 0 && v) atomicAdd(counter, v);
   }
   if (a.eval_counter) {  // evaluated find calls (fewer than the count above with primary reuse)
-    unsigned long long v = n_eval;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    unsigned long long v = w_inter;
+    if constexpr (!WAVE_COUNT) {
+      v = n_eval;
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    }
     if (lane == 0 && v) atomicAdd(a.eval_counter, v);
   }
 }

@@ -49,6 +49,17 @@ def test_stress_builds_no_join_copies(lib):
     assert [r for r in rows if r[3] != 0] == []
 
 
+@needs_llvm
+def test_repro_build_is_flagged():
+    """make repro: the bitwise-cull source with round 4's register use, the build whose all_primitives kernels
+    miscomputed on the MI355X (profiles/r05/codegen/repro.log). The detector must flag it (a positive control on a
+    real code object; the build is optional: make -C 4d_ray_tracing_amd/csrc repro)."""
+    lib = os.path.join(PKG, "lib_repro", "librt4.so")
+    _require(lib)
+    flagged = [r[0] for r in codegen_check.report(lib) if r[3] != 0]
+    assert flagged and all(name.startswith("K=33817407") for name in flagged), flagged
+
+
 def _insts(lines):
     return [(4 * k, t) for k, t in enumerate(lines)]
 

@@ -80,7 +80,8 @@ CONTROL = ("s_branch", "s_cbranch", "s_and_saveexec", "s_or_saveexec", "s_andn2_
 
 
 def split_copies_before_join(insts):
-    """Register-to-register VGPR copies placed in a join block ahead of its EXEC restore (s_or_b64 exec, exec, s[..]).
+    """Register-to-register VGPR copies (or scratch reloads) placed in a join block ahead of its EXEC restore
+    (s_or_b64 exec, exec, s[..]).
     They run only for the lanes of the branch that falls into the block; the lanes the restore re-enables skip them,
     so a live-range split whose copy-out lands there and whose copy-back runs after the restore hands those lanes
     another variable's value. Returns the offsets of such blocks."""
@@ -106,7 +107,8 @@ def split_copies_before_join(insts):
                 break
             if t2.startswith(CONTROL):
                 break
-            if VCOPY.match(t2.split("//")[0].strip()):
+            t2c = t2.split("//")[0].strip()
+            if VCOPY.match(t2c) or t2c.startswith("scratch_load"):  # a register copy or a reload of a split
                 copies += 1
     return found
 
