@@ -7,7 +7,7 @@
 // table: over L2, under the 256 MiB MALL), 128 MiB, and 1-4 GiB (far over the MALL: HBM) — and reports
 // the gather rate. Under rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum each size is one
 // dispatch, so the fabric read latency per size (LEVEL / RDREQ) can be put next to the trace kernel's
-// (profiles/r03_v33/pmc_config2.json derived.ea_read_latency_cycles).
+// (the bench-shape PMC summaries, e.g. profiles/r05_v45/pmc_config2.json derived.ea_read_latency_cycles).
 //
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/build/mall_probe tools/mall_probe.hip
 // Run:   tools/build/mall_probe [gathers_per_lane]
