@@ -47,7 +47,15 @@ using namespace rt4;
 namespace {
 
 #ifndef RT4_REFILL_MIN
-#define RT4_REFILL_MIN 1  // refill as soon as one lane is idle (A/B: 8 -> 1 is +4.5 % sphere, +6 % hypercube, +4 % tiger)
+#define RT4_REFILL_MIN 1  // refill as soon as one lane is idle (r01 A/B: 8 -> 1 is +4.5 % sphere, +6 % hypercube, +4 % tiger)
+#endif
+#ifndef RT4_REFILL_MIN_OPEN
+// The exact-count kernels without a tiger and without the lockstep rules (sphere, hypercube, cylinder4d): refill once
+// this many lanes are idle. Since the inbox (r02), the deferred exact tests (r03) and the one-trip hand-out (r04) the
+// refill's fixed cost per execution dominates its lost lanes: r05 A/B 4 / 6 / 8 against 1: config 2 -3.0 / -2.8 /
+// -3.2 %, config 3 -2.2 / -2.8 / -2.7 % kernel time; the tiger kernels lose (config 4 +0.6 %, config 5 +2.2 % at 8)
+// and keep RT4_REFILL_MIN (profiles/r05_ab.txt)
+#define RT4_REFILL_MIN_OPEN 4
 #endif
 #ifndef RT4_PHASE_REFILL
 // Lockstep for closed scenes. In a closed room every path runs all R + 1 bounces, so the
@@ -572,6 +580,9 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   constexpr bool DEFER = RT4_SPHERE_CULL && RT4_DEFER_EXACT > 0 && !POOL && !REUSE && K != GENERIC && (K & K_SPHERES) && !(K & K_TIGER) &&
                          !phase_refill_of(K) && sh_count(K, 2) != 0;
   constexpr bool PHASE = phase_refill_of(K);
+  constexpr unsigned REFILL_K =
+      K != GENERIC && (K >> 8) != 0 && !(K & K_TIGER) && !PHASE && !REUSE ? static_cast<unsigned>(RT4_REFILL_MIN_OPEN)
+                                                                          : REFILL_MIN;
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
   // Wave clock (closed scenes): while almost every path of the wave runs all R + 1 bounces
   // (early ends <= 1/32 of the sample ends, a leaky count), samples start only every R + 1 iterations, so
@@ -831,7 +842,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
     }
     if (!exhausted) {
       const unsigned long long idle = __ballot(!active);
-      bool refill = static_cast<unsigned>(__popcll(idle)) >= REFILL_MIN;
+      bool refill = static_cast<unsigned>(__popcll(idle)) >= REFILL_K;
       if (CLOCK && clock_on()) refill = refill && boundary;
       // phase-aligned: with active lanes left, wait (at most R + 1 iterations) for one of them to start
       // a sample; every active lane finishes a sample within R + 1 iterations, so the wait is bounded.
