@@ -264,6 +264,49 @@ __device__ __forceinline__ Cand tiger_cand(const rt4_scene_desc* __restrict__ S,
   return closest(lo, hi);
 }
 
+__device__ __forceinline__ V4 sel4(bool c, V4 a, V4 b) { return V4{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w}; }
+
+// One quarter q = 2 * pair + radius (pair 0: inner_cyl1 / outer_cyl1, pair 1: inner_cyl2 / outer_cyl2; radius 0:
+// inner, 1: outer) of tiger_cand, for the in-wave split of the tiger test (rt4_trace.hip TSPLIT): the pair's
+// projection and the radius-independent part of its sphere core, then the radius's early-out, asin, two faces and
+// their filters, the very ops tiger_pair runs for that radius. So
+//   tiger_cand == closest(closest(q0, q1), closest(q2, q3))
+// bit for bit (tiger_pair folds its radii the same way; closest(no_cand, x) == x, closest(x, no_cand) == x).
+// q may differ from lane to lane: the pair's geometry and the radius are selected per lane from scalar loads.
+__device__ __forceinline__ Cand tiger_quarter(const rt4_scene_desc* __restrict__ S, const SceneAux* __restrict__ X, int i,
+                                              uint32_t base, const Ray& ray, unsigned q) {
+  const rt4_tiger& t = S->tigers[i];
+  const bool pb = q >= 2u, outer = (q & 1u) != 0u;
+  const V4 pA = ld4(t.inner_cyl1.point), a1 = ld4(t.inner_cyl1.axis1), a2 = ld4(t.inner_cyl1.axis2);
+  const V4 pB = ld4(t.inner_cyl2.point), a3 = ld4(t.inner_cyl2.axis1), a4 = ld4(t.inner_cyl2.axis2);
+  const V4 cp = sel4(pb, pB, pA), ax1 = sel4(pb, a3, a1), ax2 = sel4(pb, a4, a2);
+  const V4 op = sel4(pb, pA, pB), oa1 = sel4(pb, a1, a3), oa2 = sel4(pb, a2, a4);
+  const float r = pb ? (outer ? t.outer_cyl2.r : t.inner_cyl2.r) : (outer ? t.outer_cyl1.r : t.inner_cyl1.r);
+  const DivC& d0 = X->tiger_r[i][0];
+  const DivC& d1 = X->tiger_r[i][1];
+  const DivC& d2 = X->tiger_r[i][2];
+  const DivC& d3 = X->tiger_r[i][3];
+  const DivC dc{pb ? (outer ? d3.b : d2.b) : (outer ? d1.b : d0.b), pb ? (outer ? d3.y : d2.y) : (outer ? d1.y : d0.y),
+                pb ? (outer ? d3.fast : d2.fast) : (outer ? d1.fast : d0.fast), 0};
+  const float gt = pb ? X->tiger_gt[i][1] : X->tiger_gt[i][0], lt = pb ? X->tiger_lt[i][1] : X->tiger_lt[i][0];
+  const uint32_t id = base + (pb ? 2u : 0u) + (outer ? 1u : 0u);
+  const CylProj p = cyl_project(cp, ax1, ax2, ray);
+  if (p.miss) return no_cand();
+  SphereCore2 c, c_same;
+  sphere_core_pair(cp, r, dc, r, dc, p.r12, c, c_same);  // both cores of one radius: the pair's shared part + it
+  if (c.miss) return no_cand();
+  float d_o, d_i;
+  bool f_o;
+  sphere_dist2(c, r, d_o, f_o, d_i);
+  Cand c_o{true, f_o, d_o / p.len, d_o, id};   // outer = true face
+  Cand c_i{true, false, d_i / p.len, d_i, id};  // outer = false face
+  float qd = axes_dist_sq(c_o.dist, ray, op, oa1, oa2);
+  if (qd > gt || qd < lt) c_o.hit = false;
+  qd = axes_dist_sq(c_i.dist, ray, op, oa1, oa2);
+  if (qd > gt || qd < lt) c_i.hit = false;
+  return closest(c_o, c_i);
+}
+
 // far: the ray's line clears the hypercube's ball (rt4_aux.h hyper_bound); l2 = |drct|^2
 __device__ __forceinline__ Cand cube_cand(const rt4_cube& c, const Ray& ray, uint32_t id, bool far, float l2) {  // :352-366
   const V4 cpt = ld4(c.point), cn = ld4(c.norm);

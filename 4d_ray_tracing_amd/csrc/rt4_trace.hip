@@ -112,6 +112,15 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_DEFER_TIGER
 #define RT4_DEFER_TIGER 32  // deferred tiger tests: the wave's lane threshold (rt4_trace_kernel TDEFER); 0 = off
 #endif
+#ifndef RT4_TIGER_SPLIT
+#define RT4_TIGER_SPLIT 16  // in-wave split of the tiger test in the lockstep kernels: the most lanes split (0 = off)
+#endif
+#ifndef RT4_TIGER_SPLIT_OPEN
+#define RT4_TIGER_SPLIT_OPEN 0  // the same in the open tiger kernels (tiger, all_primitives)
+#endif
+#ifndef RT4_BEAT_SLACK
+#define RT4_BEAT_SLACK 0  // in-beat tiger deferral in the lockstep kernels: parked iterations per sample (0 = off)
+#endif
 #ifndef RT4_DEFER_TIGER_WAIT
 #define RT4_DEFER_TIGER_WAIT 4
 #endif
@@ -596,7 +605,23 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   // bounding ball keeps its candidate of every other group (cold[512], pack_cand) and waits until at least
   // RT4_DEFER_TIGER lanes of the wave need the tiger test, or RT4_DEFER_TIGER_WAIT iterations; then the
   // tiger runs last, as in find_rest (closest(tiger, the rest): the same bits).
-  constexpr bool TDEFER = RT4_DEFER_TIGER > 0 && !REUSE && K != GENERIC && (K & K_TIGER) && !PHASE;
+  // In-beat deferral (RT4_BEAT_SLACK = D > 0): the lockstep kernels defer too, with the wave
+  // clock's period stretched to R + 1 + D iterations and each lane allowed at most D parked iterations per sample,
+  // so a lane that parks still ends its sample within the period and keeps the beat.
+  constexpr int BEAT_SLACK = PHASE && CLOCK ? RT4_BEAT_SLACK : 0;
+  constexpr bool TDEFER = RT4_DEFER_TIGER > 0 && !REUSE && K != GENERIC && (K & K_TIGER) && (!PHASE || BEAT_SLACK > 0);
+  int slack = BEAT_SLACK;            // BEAT_SLACK: the lane's parked iterations left in this sample
+  // In-wave split of the tiger test (RT4_TIGER_SPLIT = the most lanes split, 0 = off): when at
+  // most that many lanes of the wave need the tiger test in an iteration, each one's test is cut into its four
+  // (axes pair, radius) quarters (rt4_fast.h tiger_quarter), run on four lanes at once through a per-wave LDS
+  // hand-off, and folded back in tiger_cand's order: the same bits, on up to 4x the lanes. Lockstep kernels (the
+  // mirror room, where lanes may not park for a deferral) and, with RT4_TIGER_SPLIT_OPEN, the open ones.
+  constexpr bool TSPLIT = !REUSE && K != GENERIC && (K & K_TIGER) &&
+                          (PHASE ? RT4_TIGER_SPLIT > 0 : RT4_TIGER_SPLIT_OPEN > 0);
+  constexpr unsigned TSPLIT_MAX = PHASE ? RT4_TIGER_SPLIT : RT4_TIGER_SPLIT_OPEN;
+  static_assert(!TSPLIT || TSPLIT_MAX <= 16, "one pass of four quarters per test");
+  __shared__ float4 lds_tray[TSPLIT ? 4 * 32 : 1];  // per wave: up to 16 rays as {point, drct}
+  __shared__ float4 lds_tres[TSPLIT ? 4 * 64 : 1];  // per wave: 64 quarter results (pack_cand)
   bool tparked = false;              // TDEFER: the lane waits for the tiger test with its candidate in cold[512]
   int tdefer_age = 0;                // TDEFER, wave-uniform
   auto clock_on = [&]() { return n_early * 32u <= n_full; };
@@ -837,7 +862,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         if (__ballot(active) == 0ull) wave_it = 0;  // nothing in flight: this iteration starts the period
         boundary = wave_it == 0u;
       }
-      wave_it = wave_it + 1u == static_cast<unsigned>(R + 1) ? 0u : wave_it + 1u;
+      wave_it = wave_it + 1u == static_cast<unsigned>(R + 1 + BEAT_SLACK) ? 0u : wave_it + 1u;
       if (boundary) hold = false;
     }
     if (!exhausted) {
@@ -888,6 +913,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
               lsum_store(make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(px.y)));
               s = 0;
               b = 0;
+              if constexpr (BEAT_SLACK > 0) slack = BEAT_SLACK;
               active = NS > 0;
               pending = !active;
             }
@@ -974,7 +1000,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         c = find_rest<K>(S, X, P, ray, inter);
       }
       RT4_ACC(1, t_ph);
-    } else if constexpr (TDEFER) {
+    } else if constexpr (TDEFER || TSPLIT) {
       if (!__any(active)) {
         if (exhausted) break;
         continue;
@@ -982,7 +1008,8 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
       RT4_STAMP(t_ph);
       Cand pre = no_cand();
       bool need = false;
-      if (active) {
+      const bool held = CLOCK && parked;  // held for the wave clock (the lockstep kernels)
+      if (active && !held) {
         if (tparked) {
           pre = unpack_cand(cold[512]);
           need = true;
@@ -991,21 +1018,59 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
           need = !(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray));
         }
       }
-      const unsigned long long tm = __ballot(need);
-      const bool run = tm != 0ull && (static_cast<unsigned>(__popcll(tm)) >= static_cast<unsigned>(RT4_DEFER_TIGER) ||
-                                      tdefer_age >= RT4_DEFER_TIGER_WAIT || tm == __ballot(active));
-      if (tm != 0ull && !run) {
-        ++tdefer_age;
-        if (need) {
-          if (!tparked) cold[512] = pack_cand(pre);
-          tparked = true;
-          parked = true;
+      if constexpr (TDEFER) {
+        const unsigned long long tm = __ballot(need);
+        // in-beat: a lane with no parked iteration left forces the run (its sample must end within the period)
+        const bool forced = BEAT_SLACK > 0 && clock_on() && __ballot(need && slack <= 0) != 0ull;
+        const bool run = tm != 0ull && (static_cast<unsigned>(__popcll(tm)) >= static_cast<unsigned>(RT4_DEFER_TIGER) ||
+                                        tdefer_age >= RT4_DEFER_TIGER_WAIT || tm == __ballot(active && !held) || forced);
+        if (tm != 0ull && !run) {
+          ++tdefer_age;
+          if (need) {
+            if (!tparked) cold[512] = pack_cand(pre);
+            tparked = true;
+            parked = true;
+            if (BEAT_SLACK > 0) --slack;
+          }
+        } else {
+          tdefer_age = 0;
         }
-      } else {
-        tdefer_age = 0;
       }
-      if (active && !parked) {
-        c = need ? closest(tiger_cand(S, X, 0, prim_bases<K>(X).tiger, ray), pre) : pre;  // find_rest's last group
+      // the tiger test of the lanes that run it now (find_rest's last group: closest(tiger, the rest))
+      if constexpr (TSPLIT) {
+        const bool go = active && !parked && need;
+        Cand tg = no_cand();
+        const unsigned long long gm = __ballot(go);
+        const unsigned ng = static_cast<unsigned>(__popcll(gm));
+        if (ng > TSPLIT_MAX) {
+          if (go) tg = tiger_cand(S, X, 0, prim_bases<K>(X).tiger, ray);
+        } else if (ng != 0u) {
+          // the lanes running the test publish their rays, 4 ng lanes run the quarters, the owners fold their four
+          // results (one pass: TSPLIT_MAX <= 16; a loop of passes kept tg live across the quarter and spilled)
+          const unsigned ln = rt4_lane_id(), wv = wave_s >> 6;
+          float4* const tray = lds_tray + wv * 32u;
+          float4* const tres = lds_tres + wv * 64u;
+          const unsigned rk = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(gm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(gm), 0u));
+          if (go) {
+            tray[2u * rk] = make_float4(ray.point.x, ray.point.y, ray.point.z, ray.point.w);
+            tray[2u * rk + 1u] = make_float4(ray.drct.x, ray.drct.y, ray.drct.z, ray.drct.w);
+          }
+          if (ln < 4u * ng) {  // quarter ln & 3 of the test of the lane ranked ln >> 2
+            const float4 p4 = tray[2u * (ln >> 2)], d4 = tray[2u * (ln >> 2) + 1u];
+            tres[ln] = pack_cand(tiger_quarter(S, X, 0, prim_bases<K>(X).tiger,
+                                               Ray{V4{p4.x, p4.y, p4.z, p4.w}, V4{d4.x, d4.y, d4.z, d4.w}}, ln & 3u));
+          }
+          if (go)
+            tg = closest(closest(unpack_cand(tres[4u * rk]), unpack_cand(tres[4u * rk + 1u])),
+                         closest(unpack_cand(tres[4u * rk + 2u]), unpack_cand(tres[4u * rk + 3u])));
+        }
+        if (active && !parked) {
+          c = need ? closest(tg, pre) : pre;
+          tparked = false;
+        }
+      } else if (active && !parked) {
+        c = need ? closest(tiger_cand(S, X, 0, prim_bases<K>(X).tiger, ray), pre) : pre;
         tparked = false;
       }
       RT4_ACC(1, t_ph);
@@ -1078,6 +1143,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
           ray = Ray{focus, V4{c0.x, c0.y, c0.z, c0.w}};
           ++s;
           b = 0;
+          if constexpr (BEAT_SLACK > 0) slack = BEAT_SLACK;
           acc = V3{0.0f, 0.0f, 0.0f};
           T = V3{1.0f, 1.0f, 1.0f};
           if (s >= NS) {
