@@ -619,9 +619,16 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   constexpr bool TSPLIT = !REUSE && K != GENERIC && (K & K_TIGER) &&
                           (PHASE ? RT4_TIGER_SPLIT > 0 : RT4_TIGER_SPLIT_OPEN > 0);
   constexpr unsigned TSPLIT_MAX = PHASE ? RT4_TIGER_SPLIT : RT4_TIGER_SPLIT_OPEN;
+  // Open tiger kernels (TDEFER and TSPLIT): a run serves at most TSPLIT_MAX lanes, the parked ones first, and the
+  // others stay parked, so every test runs split and the direct test is not compiled. Their rays and results move by
+  // ds_bpermute (no LDS buffer: the all_primitives kernel's LDS allows no more at 6 blocks per CU). Bit-exact
+  // (tools/variant_probe.py) but rejected (profiles/r05_ab.txt, r05-v48 trial): the per-lane pair geometry takes
+  // ~40 VGPRs, so the kernel spills at 6 waves and runs 5 (-6.9 % config 5, 20 B spill) or 4 (-12 %, no spill).
+  constexpr bool TSERVE = TSPLIT && TDEFER && !PHASE;
   static_assert(!TSPLIT || TSPLIT_MAX <= 16, "one pass of four quarters per test");
-  __shared__ float4 lds_tray[TSPLIT ? 4 * 32 : 1];  // per wave: up to 16 rays as {point, drct}
-  __shared__ float4 lds_tres[TSPLIT ? 4 * 64 : 1];  // per wave: 64 quarter results (pack_cand)
+  __shared__ float4 lds_tray[TSPLIT && !TSERVE ? 4 * 32 : 1];  // per wave: up to 16 rays as {point, drct}
+  __shared__ float4 lds_tres[TSPLIT && !TSERVE ? 4 * 64 : 1];  // per wave: 64 quarter results (pack_cand)
+  __shared__ uint32_t lds_town[TSERVE ? 4 * 16 : 1];            // per wave: the lane of each served test
   bool tparked = false;              // TDEFER: the lane waits for the tiger test with its candidate in cold[512]
   int tdefer_age = 0;                // TDEFER, wave-uniform
   auto clock_on = [&]() { return n_early * 32u <= n_full; };
@@ -1018,7 +1025,25 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
           need = !(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray));
         }
       }
-      if constexpr (TDEFER) {
+      if constexpr (TSERVE) {
+        const unsigned long long mp = __ballot(need && tparked), mn = __ballot(need && !tparked);
+        const unsigned np = static_cast<unsigned>(__popcll(mp)), nt = np + static_cast<unsigned>(__popcll(mn));
+        const bool run = nt != 0u && (nt >= static_cast<unsigned>(RT4_DEFER_TIGER) || tdefer_age >= RT4_DEFER_TIGER_WAIT ||
+                                      (mp | mn) == __ballot(active && !held));
+        const unsigned slot = tparked ? __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mp >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mp), 0u))
+                                      : np + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mn >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mn), 0u));
+        const bool serve = run && need && slot < TSPLIT_MAX;  // the parked lanes first, at most TSPLIT_MAX
+        // every lane's candidate waits in cold[512] (no VGPRs held across the split test)
+        if (active && !held && !tparked) cold[512] = pack_cand(pre);
+        if (need && !serve) {
+          tparked = true;
+          parked = true;
+        }
+        // a run that left lanes parked runs again next iteration; otherwise the deferral's clock
+        tdefer_age = run ? (nt > TSPLIT_MAX ? RT4_DEFER_TIGER_WAIT : 0) : (nt != 0u ? tdefer_age + 1 : 0);
+      } else if constexpr (TDEFER) {
         const unsigned long long tm = __ballot(need);
         // in-beat: a lane with no parked iteration left forces the run (its sample must end within the period)
         const bool forced = BEAT_SLACK > 0 && clock_on() && __ballot(need && slack <= 0) != 0ull;
@@ -1037,7 +1062,47 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         }
       }
       // the tiger test of the lanes that run it now (find_rest's last group: closest(tiger, the rest))
-      if constexpr (TSPLIT) {
+#ifdef RT4_LANESTATS  // diagnostic: tiger tests and their lanes (counter[60], [61]), as find_rest counts them
+      {
+        const unsigned long long gm_ = __ballot(active && !parked && need);
+        if (gm_ && lane == static_cast<unsigned>(__builtin_ctzll(__builtin_amdgcn_read_exec()))) {
+          atomicAdd(counter + 60, 1ull);
+          atomicAdd(counter + 61, static_cast<unsigned long long>(__popcll(gm_)));
+        }
+      }
+#endif
+      if constexpr (TSERVE) {
+        // every served test split into its quarters; rays and results by ds_bpermute, the owners' lanes by LDS
+        const bool go = active && !parked && need;
+        const unsigned long long gm = __ballot(go);
+        const unsigned ng = static_cast<unsigned>(__popcll(gm));
+        Cand tg = no_cand();
+        if (ng != 0u) {
+          const unsigned ln = rt4_lane_id(), wv = wave_s >> 6;
+          const unsigned rk = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(gm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(gm), 0u));
+          if (go) lds_town[wv * 16u + rk] = ln;
+          const bool task = ln < 4u * ng;
+          const int src = static_cast<int>((task ? lds_town[wv * 16u + (ln >> 2)] : ln) << 2);
+          auto pull = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v))); };
+          const Ray tr{V4{pull(ray.point.x), pull(ray.point.y), pull(ray.point.z), pull(ray.point.w)},
+                       V4{pull(ray.drct.x), pull(ray.drct.y), pull(ray.drct.z), pull(ray.drct.w)}};
+          float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (task) q = pack_cand(tiger_quarter(S, X, 0, prim_bases<K>(X).tiger, tr, ln & 3u));
+          auto part = [&](unsigned j) {  // the owner's quarter j, from lane 4 rk + j
+            const int from = static_cast<int>(((go ? 4u * rk + j : ln) & 63u) << 2);
+            return unpack_cand(make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(q.x))),
+                                           __int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(q.y))),
+                                           __int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(q.z))), 0.0f));
+          };
+          const Cand t01 = closest(part(0u), part(1u));
+          tg = closest(t01, closest(part(2u), part(3u)));
+        }
+        if (active && !parked) {
+          c = go ? closest(tg, unpack_cand(cold[512])) : unpack_cand(cold[512]);
+          tparked = false;
+        }
+      } else if constexpr (TSPLIT) {
         const bool go = active && !parked && need;
         Cand tg = no_cand();
         const unsigned long long gm = __ballot(go);
