@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
       const unsigned gq = a.fcolor ? (pk >> 26) & 0x3F : (pk >> 30) & 3;
       const unsigned gn = a.fcolor && a.n_jobs == 1 ? static_cast<unsigned>(a.n_frames) : static_cast<unsigned>(a.n_jobs);
       const rt4_region& grg = a.jobs[gq < static_cast<unsigned>(a.n_jobs) ? gq : 0].reg;
-      if (gq < gn && gj < static_cast<unsigned>(grg.w) && gi < static_cast<unsigned>(grg.h))
+      if (gq < gn && gj < static_cast<unsigned>(grg.w) && gi < static_cast<unsigned>(grg.h)) {
 #endif
       if (a.fcolor) {
         // pipelined or overlapped frames: the light sum of frame f as is; rt4_fold_frames_kernel tone-maps and
@@ -742,6 +742,9 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         for (int jb = 0; jb < a.n_jobs; jb++)
           if (((pk >> 30) & 3) == jb) write_pixel<REMAT>(a, a.jobs[jb], pk, V3{lp.x, lp.y, lp.z});
       }
+#ifdef RT4_GUARD_WRITES
+      }
+#endif
     }
     ring_n = 0;
   };
