@@ -14,6 +14,9 @@
 #ifndef RT4_SPHERE_CULL
 #define RT4_SPHERE_CULL 1
 #endif
+#ifndef RT4_HYPER_AXIS_TIGER
+#define RT4_HYPER_AXIS_TIGER 0  // the axis form in the tiger kernels too (A/B knob)
+#endif
 #ifndef RT4_HYPER_AXIS
 #define RT4_HYPER_AXIS 1  // hypercube cull: one-component form for axis-aligned canonical cells (rt4_aux.h
                           // hyper_axis); not in the tiger kernels, where it measured 4.5 % slower
@@ -599,7 +602,7 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
     });
   if (K & K_UNION)
     if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && !(K & K_TIGER)>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
+  if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && (RT4_HYPER_AXIS_TIGER || !(K & K_TIGER))>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
   if ((K & K_TIGER) && WITH_TIGER)
     if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) {
 #ifdef RT4_LANESTATS  // diagnostic: tiger tests and their active lanes (counter[60], [61])
