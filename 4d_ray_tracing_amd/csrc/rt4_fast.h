@@ -15,11 +15,12 @@
 #define RT4_SPHERE_CULL 1
 #endif
 #ifndef RT4_HYPER_AXIS_TIGER
-#define RT4_HYPER_AXIS_TIGER 0  // the axis form in the tiger kernels too (A/B knob)
+#define RT4_HYPER_AXIS_TIGER 1  // the axis form in the tiger kernels too: r05-v48, config 5 +4.3 % (r05_ab.txt); it
+                                // measured 4.5 % slower before r05-v45's register savings
 #endif
 #ifndef RT4_HYPER_AXIS
 #define RT4_HYPER_AXIS 1  // hypercube cull: one-component form for axis-aligned canonical cells (rt4_aux.h
-                          // hyper_axis); not in the tiger kernels, where it measured 4.5 % slower
+                          // hyper_axis)
 #endif
 #ifndef RT4_HYPER_PENDING
 #define RT4_HYPER_PENDING 1  // hypercube: per-lane pending-cell loop (hypercube_cand) instead of 8 cells in order

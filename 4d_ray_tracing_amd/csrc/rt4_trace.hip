@@ -171,6 +171,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_SIDE_LOW_PRIORITY
 #define RT4_SIDE_LOW_PRIORITY 1  // overlapped traces on streams made with the least priority (measured 2-5 % faster)
 #endif
+#ifndef RT4_FOLD_PRIO
+#define RT4_FOLD_PRIO 3  // wave priority of the fold kernel (s_setprio): overlapped frames -0.5..-0.9 % (r05-v48)
+#endif
 #ifndef RT4_OVERLAP_SLOTS
 // Overlapped launches in flight at once: RT4_OVERLAP_SLOTS (and as many side streams) for frames too small to fill
 // the chip, RT4_OVERLAP_BIG for the others (more streams than the process's four hardware queues cost a frame that
@@ -1484,6 +1487,10 @@ __global__ void rt4_tile_order_kernel(const rt4_scene_desc* __restrict__ S, cons
 // count_src (an overlapped single frame): the trace kernel's count, moved into the caller's counter here, on
 // the caller's stream, and reset for the slot's next frame
 __global__ void rt4_fold_frames_kernel(const KernelArgs a, unsigned long long* count_src, unsigned long long* count_dst) {
+#if RT4_FOLD_PRIO > 0
+  // the fold's waves win the SIMD's issue arbitration over the co-resident trace waves of later frames
+  __builtin_amdgcn_s_setprio(RT4_FOLD_PRIO);
+#endif
   const int job = static_cast<int>(blockIdx.y);  // the section of an overlapped sections launch (else 0)
   const JobArgs& J = a.jobs[job];
   const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
