@@ -115,6 +115,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_TIGER_SPLIT
 #define RT4_TIGER_SPLIT 16  // in-wave split of the tiger test in the lockstep kernels: the most lanes split (0 = off)
 #endif
+#ifndef RT4_TIGER_SPLIT_REUSE
+#define RT4_TIGER_SPLIT_REUSE 1  // the split in the lockstep kernels' primary-reuse instantiations too
+#endif
 #ifndef RT4_TIGER_SPLIT_OPEN
 #define RT4_TIGER_SPLIT_OPEN 0  // the same in the open tiger kernels (tiger, all_primitives)
 #endif
@@ -619,7 +622,8 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   // (axes pair, radius) quarters (rt4_fast.h tiger_quarter), run on four lanes at once through a per-wave LDS
   // hand-off, and folded back in tiger_cand's order: the same bits, on up to 4x the lanes. Lockstep kernels (the
   // mirror room, where lanes may not park for a deferral) and, with RT4_TIGER_SPLIT_OPEN, the open ones.
-  constexpr bool TSPLIT = !REUSE && K != GENERIC && (K & K_TIGER) &&
+  // (with primary reuse only in the lockstep kernels: a lane whose bounce 0 comes from the cache takes no part)
+  constexpr bool TSPLIT = (!REUSE || (CLOCK && RT4_TIGER_SPLIT_REUSE)) && K != GENERIC && (K & K_TIGER) &&
                           (PHASE ? RT4_TIGER_SPLIT > 0 : RT4_TIGER_SPLIT_OPEN > 0);
   constexpr unsigned TSPLIT_MAX = PHASE ? RT4_TIGER_SPLIT : RT4_TIGER_SPLIT_OPEN;
   // Open tiger kernels (TDEFER and TSPLIT): a run serves at most TSPLIT_MAX lanes, the parked ones first, and the
@@ -1023,7 +1027,13 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
       bool need = false;
       const bool held = CLOCK && parked;  // held for the wave clock (the lockstep kernels)
       if (active && !held) {
-        if (tparked) {
+        if constexpr (CLOCK && REUSE) {  // as the generic path below: bounce 0 from the cache at the clock boundary
+          cached = use_cached;
+          use_cached = false;
+        }
+        if (cached) {
+          pre = unpack_cand(cold[512]);
+        } else if (tparked) {
           pre = unpack_cand(cold[512]);
           need = true;
         } else {
