@@ -63,6 +63,12 @@ struct alignas(32) SphereCull {
   float pad[2];
 };
 
+// The same cull for the 2-axis cylinders (rt4_fast.h cyl_cand_cull): their exact test is sphere_cand on the ray
+// projected onto the cylinder's 2-plane (shader.frag:251-267), and the derivation above is in terms of d2 and
+// dot_pord alone, whatever the ray's direction, so it holds for the projected ray as it is. Only d2_out and r2m
+// are used (the centre is the cylinder's point). A tiger's axes pair skips its shared sphere core when both of its
+// radii cull; one quarter of the in-wave split when its own radius does.
+
 // Bounding hypersphere of a tiger / cylinders union (rt4_fast.h far_from): every point the exact test
 // can report as a hit lies on one cylinder (distance r from its axes plane, up to ~1e-5 relative) and
 // passes the other cylinder's axes-distance filter (d^2 <= gt). When the two axes planes are
@@ -135,6 +141,11 @@ struct SceneAux {
   // primitive table so the pending-cell loop can read the cell a lane needs (rt4_fast.h)
   float hyper_cells[8][24];  // must directly precede prims (kernels address it as prims - 48 float4)
   PrimEntry prims[MAX_PRIMS];
+  // after the table, so that the fields above keep their offsets (r05-v50; the kernels' scalar addressing and so
+  // their schedules stay as they were)
+  SphereCull cyl_cull[RT4_MAX_CYLINDERS];
+  SphereCull union_cull[RT4_MAX_UNIONS][2];
+  SphereCull tiger_cull[RT4_MAX_TIGERS][4];  // inner_cyl1, outer_cyl1, inner_cyl2, outer_cyl2 (as tiger_r)
 };
 
 static_assert(offsetof(SceneAux, prims) - offsetof(SceneAux, hyper_cells) == sizeof(float) * 8 * 24,

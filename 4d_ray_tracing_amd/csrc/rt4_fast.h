@@ -191,6 +191,30 @@ __device__ __forceinline__ Cand cyl_cand(const CylProj& p, V4 cp, float r, const
   return c;
 }
 
+// cyl_cand with the sphere cull (rt4_aux.h SphereCull) on the projected ray: a lane whose projected line clears
+// the circle skips the transcendental part; the exact part reuses the cull's two dots (sphere_cand_d: the same
+// ops on the same operands as sphere_cand), so the result is cyl_cand's, bit for bit.
+__device__ __forceinline__ bool sphere_culled(float d2, float dp, float d2_out, float r2m) {
+  return d2 >= d2_out && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, r2m));
+}
+__device__ __forceinline__ Cand cyl_cand_cull(const CylProj& p, V4 cp, float r, const DivC& dc, const SphereCull& k,
+                                              bool outer, uint32_t id) {
+  if (p.miss) return no_cand();
+  const V4 po = sub(cp, p.r12.point);
+  const float d2 = dot(po, po), dp = dot(po, p.r12.drct);
+  if (sphere_culled(d2, dp, k.d2_out, k.r2m)) return no_cand();
+  Cand c = sphere_cand_d(d2, dp, r, dc, outer, id);
+  c.dist = c.dist / p.len;  // inter.dist /= drct_in_plane_length (:265)
+  return c;
+}
+#ifndef RT4_CYL_CULL
+#define RT4_CYL_CULL 1  // the sphere cull for the cylinders and the union's cylinders (A/B knob)
+#endif
+#ifndef RT4_TIGER_CULL
+#define RT4_TIGER_CULL 0  // the sphere cull for the tiger's axes pairs and split quarters: config 4 -1.3 %, config 5
+                          // +-0 (r05_ab.txt), off
+#endif
+
 // dist_to_axes_plane(..)^2 without the sqrt (shader.frag:270-275)
 __device__ __forceinline__ float axes_dist_sq(float dist, const Ray& ray, V4 cp, V4 a1, V4 a2) {
   const V4 p = mad(ray.drct, dist, ray.point);
@@ -206,9 +230,19 @@ __device__ __forceinline__ Cand union_cand(const rt4_scene_desc* __restrict__ S,
   const V4 p1 = ld4(u.cylinder1.point), a11 = ld4(u.cylinder1.axis1), a12 = ld4(u.cylinder1.axis2);
   const V4 p2 = ld4(u.cylinder2.point), a21 = ld4(u.cylinder2.axis1), a22 = ld4(u.cylinder2.axis2);
   const float gt = X->union_gt[i];
+#if RT4_CYL_CULL
+  Cand c1 = cyl_cand_cull(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], X->union_cull[i][0], true,
+                          base);
+#else
   Cand c1 = cyl_cand(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], true, base);
+#endif
   if (c1.hit && axes_dist_sq(c1.dist, ray, p2, a21, a22) > gt) c1.hit = false;
+#if RT4_CYL_CULL
+  Cand c2 = cyl_cand_cull(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], X->union_cull[i][1], true,
+                          base + 1);
+#else
   Cand c2 = cyl_cand(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], true, base + 1);
+#endif
   if (c2.hit && axes_dist_sq(c2.dist, ray, p1, a11, a12) > gt) c2.hit = false;
   return closest(c1, c2);
 }
@@ -217,9 +251,17 @@ __device__ __forceinline__ Cand union_cand(const rt4_scene_desc* __restrict__ S,
 // outer = true/false, kept iff the other pair's axes distance d satisfies lt <= d^2 <= gt.
 __device__ __forceinline__ Cand tiger_pair(V4 cp, V4 a1, V4 a2, float r_in, float r_out, const DivC& dc_in,
                                            const DivC& dc_out, V4 op, V4 oa1, V4 oa2, float gt, float lt,
-                                           const Ray& ray, uint32_t id_base) {
+                                           const Ray& ray, uint32_t id_base, const SphereCull& k_in,
+                                           const SphereCull& k_out) {
   const CylProj p = cyl_project(cp, a1, a2, ray);
   if (p.miss) return no_cand();
+#if RT4_TIGER_CULL
+  {  // both radii miss (rt4_aux.h SphereCull): no face of this pair can hit
+    const V4 po = sub(cp, p.r12.point);
+    const float d2 = dot(po, po), dp = dot(po, p.r12.drct);
+    if (sphere_culled(d2, dp, k_in.d2_out, k_in.r2m) && sphere_culled(d2, dp, k_out.d2_out, k_out.r2m)) return no_cand();
+  }
+#endif
   SphereCore2 c_in, c_out;
   sphere_core_pair(cp, r_in, dc_in, r_out, dc_out, p.r12, c_in, c_out);
   Cand res = no_cand();
@@ -262,9 +304,10 @@ __device__ __forceinline__ Cand tiger_cand(const rt4_scene_desc* __restrict__ S,
   const V4 pA = ld4(t.inner_cyl1.point), a1 = ld4(t.inner_cyl1.axis1), a2 = ld4(t.inner_cyl1.axis2);
   const V4 pB = ld4(t.inner_cyl2.point), a3 = ld4(t.inner_cyl2.axis1), a4 = ld4(t.inner_cyl2.axis2);
   const Cand lo = tiger_pair(pA, a1, a2, t.inner_cyl1.r, t.outer_cyl1.r, X->tiger_r[i][0], X->tiger_r[i][1], pB, a3,
-                             a4, X->tiger_gt[i][0], X->tiger_lt[i][0], ray, base);
+                             a4, X->tiger_gt[i][0], X->tiger_lt[i][0], ray, base, X->tiger_cull[i][0], X->tiger_cull[i][1]);
   const Cand hi = tiger_pair(pB, a3, a4, t.inner_cyl2.r, t.outer_cyl2.r, X->tiger_r[i][2], X->tiger_r[i][3], pA, a1,
-                             a2, X->tiger_gt[i][1], X->tiger_lt[i][1], ray, base + 2);
+                             a2, X->tiger_gt[i][1], X->tiger_lt[i][1], ray, base + 2, X->tiger_cull[i][2],
+                             X->tiger_cull[i][3]);
   return closest(lo, hi);
 }
 
@@ -296,6 +339,18 @@ __device__ __forceinline__ Cand tiger_quarter(const rt4_scene_desc* __restrict__
   const uint32_t id = base + (pb ? 2u : 0u) + (outer ? 1u : 0u);
   const CylProj p = cyl_project(cp, ax1, ax2, ray);
   if (p.miss) return no_cand();
+#if RT4_TIGER_CULL
+  {  // this radius misses (rt4_aux.h SphereCull)
+    const SphereCull& k0 = X->tiger_cull[i][0];
+    const SphereCull& k1 = X->tiger_cull[i][1];
+    const SphereCull& k2 = X->tiger_cull[i][2];
+    const SphereCull& k3 = X->tiger_cull[i][3];
+    const float kd = pb ? (outer ? k3.d2_out : k2.d2_out) : (outer ? k1.d2_out : k0.d2_out);
+    const float kr = pb ? (outer ? k3.r2m : k2.r2m) : (outer ? k1.r2m : k0.r2m);
+    const V4 po = sub(cp, p.r12.point);
+    if (sphere_culled(dot(po, po), dot(po, p.r12.drct), kd, kr)) return no_cand();
+  }
+#endif
   SphereCore2 c, c_same;
   sphere_core_pair(cp, r, dc, r, dc, p.r12, c, c_same);  // both cores of one radius: the pair's shared part + it
   if (c.miss) return no_cand();
@@ -597,9 +652,15 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
     for_count<NCY>(S->n_cylinders, [&](int i) {
       const rt4_cylinder& c = S->cylinders[i];
       const V4 cp = ld4(c.point);
+#if RT4_CYL_CULL
+      inter = closest(cyl_cand_cull(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], X->cyl_cull[i],
+                                    true, B.cyl + static_cast<uint32_t>(i)),
+                      inter);
+#else
       inter = closest(cyl_cand(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], true,
                                B.cyl + static_cast<uint32_t>(i)),
                       inter);
+#endif
     });
   if (K & K_UNION)
     if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);

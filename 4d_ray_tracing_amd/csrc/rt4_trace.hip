@@ -198,6 +198,9 @@ static_assert(RT4_OVERLAP_BIG >= 2 && RT4_OVERLAP_BIG <= RT4_OVERLAP_SLOTS, "ove
 #ifndef RT4_WAVES_MIRROR
 #define RT4_WAVES_MIRROR 6  // the tiger kernel specialised for three or more spaces (config 4's mirror room)
 #endif
+#ifndef RT4_WAVES_MIRROR_INLINE
+#define RT4_WAVES_MIRROR_INLINE 6  // the same with the inline Newton sampler (5 with RT4_TIGER_CULL: one spill at 6)
+#endif
 #ifndef RT4_WAVES_MIRROR_REUSE
 #define RT4_WAVES_MIRROR_REUSE 5  // its primary-reuse instantiations (spilled in the loop at 6)
 #endif
@@ -528,7 +531,8 @@ constexpr int min_waves_of(uint32_t K, bool reuse = false, bool lut = true) {
   if ((K >> 8) == 0) return RT4_WAVES_PER_SIMD;  // runtime counts: the allocator's choice (no spill)
   if (K & (K_SPHERES | K_CYLINDERS | K_UNION | K_HYPERCUBE))
     return reuse ? RT4_WAVES_ALLPRIM_REUSE : (lut ? RT4_WAVES_ALLPRIM : RT4_WAVES_ALLPRIM_INLINE);
-  if (((K >> 8) & 0xFFu) >= 4) return reuse ? RT4_WAVES_MIRROR_REUSE : RT4_WAVES_MIRROR;  // SH(): space count + 1, bits 8..15
+  if (((K >> 8) & 0xFFu) >= 4)  // SH(): space count + 1, bits 8..15
+    return reuse ? RT4_WAVES_MIRROR_REUSE : (lut ? RT4_WAVES_MIRROR : RT4_WAVES_MIRROR_INLINE);
   return RT4_WAVES_PER_SIMD;
 }
 
@@ -1078,12 +1082,16 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         }
       }
       // the tiger test of the lanes that run it now (find_rest's last group: closest(tiger, the rest))
-#ifdef RT4_LANESTATS  // diagnostic: tiger tests and their lanes (counter[60], [61]), as find_rest counts them
+#ifdef RT4_LANESTATS  // diagnostic: tiger tests and their lanes (counter[60], [61], [64..71]), as find_rest counts them
       {
         const unsigned long long gm_ = __ballot(active && !parked && need);
         if (gm_ && lane == static_cast<unsigned>(__builtin_ctzll(__builtin_amdgcn_read_exec()))) {
           atomicAdd(counter + 60, 1ull);
           atomicAdd(counter + 61, static_cast<unsigned long long>(__popcll(gm_)));
+          // by lanes: 1-16, 17-32, 33-48, 49-64 (counter[64..67] events, [68..71] lanes; tools/lanestats.py)
+          const unsigned bk_ = (static_cast<unsigned>(__popcll(gm_)) - 1u) >> 4;
+          atomicAdd(counter + 64 + bk_, 1ull);
+          atomicAdd(counter + 68 + bk_, static_cast<unsigned long long>(__popcll(gm_)));
         }
       }
 #endif
@@ -1855,18 +1863,24 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
   }
   int st = RT4_OK;
   for (int i = 0; i < s.n_spheres; i++) a->sphere_r[i] = make_divc(s.spheres[i].r);
-  for (int i = 0; i < s.n_spheres; i++) {  // rt4_aux.h SphereCull
-    const float r = s.spheres[i].r;
-    std::memcpy(a->sphere_cull[i].center, s.spheres[i].center, sizeof a->sphere_cull[i].center);
+  auto cull_of = [](float r, const float* center, SphereCull* k) {  // rt4_aux.h SphereCull
+    std::memset(k, 0, sizeof *k);
+    std::memcpy(k->center, center, sizeof k->center);
     // SMALL_F, shader.frag:24; a NaN radius never takes the exact early-out (len_po >= NaN is false)
-    a->sphere_cull[i].d2_out = std::isnan(r) ? NAN : sqrt_lt_threshold(std::max(r, 0.0003f));
+    k->d2_out = std::isnan(r) ? NAN : sqrt_lt_threshold(std::max(r, 0.0003f));
     const bool ok = r >= 1e-15f && r <= 1e15f;  // r <= 0: sin_oap < 1 always, never cull
-    a->sphere_cull[i].r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
+    k->r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
+  };
+  for (int i = 0; i < s.n_spheres; i++) cull_of(s.spheres[i].r, s.spheres[i].center, &a->sphere_cull[i]);
+  for (int i = 0; i < s.n_cylinders; i++) {
+    a->cyl_r[i] = make_divc(s.cylinders[i].r);
+    cull_of(s.cylinders[i].r, s.cylinders[i].point, &a->cyl_cull[i]);
   }
-  for (int i = 0; i < s.n_cylinders; i++) a->cyl_r[i] = make_divc(s.cylinders[i].r);
   for (int i = 0; i < s.n_unions; i++) {
     a->union_r[i][0] = make_divc(s.unions[i].cylinder1.r);
     a->union_r[i][1] = make_divc(s.unions[i].cylinder2.r);
+    cull_of(s.unions[i].cylinder1.r, s.unions[i].cylinder1.point, &a->union_cull[i][0]);
+    cull_of(s.unions[i].cylinder2.r, s.unions[i].cylinder2.point, &a->union_cull[i][1]);
     a->union_gt[i] = sqrt_gt_threshold(s.unions[i].cylinder2.r);
   }
   // bounding balls (rt4_aux.h BoundBall): R^2 = max over faces (r_self^2 + gt of the filter)
@@ -1968,6 +1982,8 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     const rt4_tiger& t = s.tigers[i];
     const float rs[4] = {t.inner_cyl1.r, t.outer_cyl1.r, t.inner_cyl2.r, t.outer_cyl2.r};
     for (int k = 0; k < 4; k++) a->tiger_r[i][k] = make_divc(rs[k]);
+    const float* cps[4] = {t.inner_cyl1.point, t.outer_cyl1.point, t.inner_cyl2.point, t.outer_cyl2.point};
+    for (int k = 0; k < 4; k++) cull_of(rs[k], cps[k], &a->tiger_cull[i][k]);
     a->tiger_gt[i][0] = sqrt_gt_threshold(t.outer_cyl2.r);
     a->tiger_lt[i][0] = sqrt_lt_threshold(t.inner_cyl2.r);
     a->tiger_gt[i][1] = sqrt_gt_threshold(t.outer_cyl1.r);

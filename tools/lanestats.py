@@ -4,7 +4,7 @@
 Usage: RT4_LIB=<lanestats .so> python tools/lanestats.py [scene] [spp] [bounces] [W] [H] [frames] [mode]
   mode: "pipelined" (frames in one rt4_render_frames_device call) or "fbf" (one launch per frame).
 The counters accumulate over every launch of the run (counter[16..] per phase, counter[40..41] exact
-sphere trips)."""
+sphere trips, counter[60..71] tiger tests)."""
 import importlib
 import os
 import sys
@@ -25,7 +25,7 @@ mode = a[6] if len(a) > 6 else "fbf"
 t = rt4.Tracer(0, rt4.FLAG_SAMPLER_LUT | int(os.environ.get("RT4_EXTRA_FLAGS", "0"), 0), rt4.Scene.named(scene))
 u = rt4.make_uniforms(W, H, samples=spp, reflections=bounces, seed=12345)
 frame = torch.zeros((H, W, 4), device="cuda")
-cnt = torch.zeros(64, dtype=torch.int64, device="cuda")
+cnt = torch.zeros(80, dtype=torch.int64, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 if mode == "pipelined" and frames > 1:
@@ -58,6 +58,11 @@ if c[58]:
 if c[60]:
     print(f"  {'tiger test':>30s}: {c[60]:12d} wave execs ({c[60] / max(c[16], 1):5.3f} per iteration), "
           f"{c[61] / c[60]:5.1f} lanes avg")
+if any(c[64:68]):
+    print("  tiger tests by lanes needing them (share of tests, lanes avg):")
+    for k, lab in enumerate(["1-16", "17-32", "33-48", "49-64"]):
+        if c[64 + k]:
+            print(f"    {lab:>6s}: {c[64 + k] / c[60]:6.3f}  {c[68 + k] / c[64 + k]:5.1f}")
 if any(c[42:49]):
     tot = sum(c[42:49])
     print("  finds with pending spheres, by lanes pending (wave events share, lanes avg):")
