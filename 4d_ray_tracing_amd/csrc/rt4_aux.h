@@ -60,7 +60,8 @@ struct alignas(32) SphereCull {
   float center[4];  // spheres[i].center
   float d2_out;     // smallest d2 with RN(sqrt(d2)) >= max(r, SMALL_F)
   float r2m;        // RN(r^2 (1 + 1e-4)); +inf disables the cull (tiny or non-finite r)
-  float pad[2];
+  float r2m_pre;    // r2m (1 + 1e-6), rounded up: the cylinders' pre-normalisation cull (below); +inf disables
+  float pad;
 };
 
 // The same cull for the 2-axis cylinders (rt4_fast.h cyl_cand_cull): their exact test is sphere_cand on the ray
@@ -68,6 +69,18 @@ struct alignas(32) SphereCull {
 // dot_pord alone, whatever the ray's direction, so it holds for the projected ray as it is. Only d2_out and r2m
 // are used (the centre is the cylinder's point). A tiger's axes pair skips its shared sphere core when both of its
 // radii cull; one quarter of the in-wave split when its own radius does.
+// Pre-normalisation form (rt4_fast.h cyl_cand_precull): cyl_project normalises the projected direction e (two
+// lengths, four divisions) before the test needs dp = dot(po, RN(e / len)). With u = 2^-24, |dp - s| <= 8.1u sqrt(d2)
+// for s = dot(po, e) / |e| (the division and sqrt round once each, the two dots by gamma_4), so
+//   P = RN(d2 - RN(dp^2)) >= d2 - s^2 - 18.2u d2,   T = RN(fma(K, d2, r2m)) <= (K d2 + r2m)(1 + u),
+// and P > T (the cull above, hence the miss) follows from d2 - s^2 > (K + 18.3u) d2 + r2m (1 + u)   (1).
+// From Q = dot(po, e), L = dot(e, e) (relative error gamma_4 for L, 4u sqrt(d2) |e| for Q) and M = d2 |e|^2:
+//   lhs = RN(RN(d2 L) - RN(Q^2)) <= M - (po.e)^2 + 15.1u M,   rhs = RN(RN(fma(K2, d2, r2m_pre)) L)
+//   >= (K2 d2 + r2m_pre) |e|^2 (1 - 6.1u),
+// so lhs > rhs gives d2 - s^2 > (K2 (1 - 6.1u) - 15.1u) d2 + r2m_pre (1 - 6.1u), which implies (1) for
+// K2 >= K + 33.4u (~6.0e-6; CYL_PRECULL_K = 8e-6) and r2m_pre >= r2m (1 + 7.2u). The operands are kept in range
+// (d2, L < 1e18, L > 1e-30; d2 >= d2_out > 9e-8) so that no product overflows or leaves the normal range.
+constexpr float CYL_PRECULL_K = 8e-6f;
 
 // Bounding hypersphere of a tiger / cylinders union (rt4_fast.h far_from): every point the exact test
 // can report as a hit lies on one cylinder (distance r from its axes plane, up to ~1e-5 relative) and

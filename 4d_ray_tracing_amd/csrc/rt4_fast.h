@@ -207,8 +207,38 @@ __device__ __forceinline__ Cand cyl_cand_cull(const CylProj& p, V4 cp, float r, 
   c.dist = c.dist / p.len;  // inter.dist /= drct_in_plane_length (:265)
   return c;
 }
+// cyl_project + cyl_cand_cull with the cull tested first on the unnormalised projected direction (rt4_aux.h
+// SphereCull, pre-normalisation form): a culled lane skips the two lengths and four divisions too. The lanes it
+// does not cull take cyl_project's remaining steps and cyl_cand_cull's test and exact part, the same ops on the
+// same operands, so the result is cyl_cand's, bit for bit.
+__device__ __forceinline__ Cand cyl_cand_precull(V4 cp, V4 a1, V4 a2, const Ray& ray, float r, const DivC& dc,
+                                                 const SphereCull& k, bool outer, uint32_t id) {
+  const V4 r1p = point_in_space(ray.point, cp, a1), r1d = vec_in_space(ray.drct, a1);
+  const V4 p12 = point_in_space(r1p, cp, a2), e = vec_in_space(r1d, a2);
+  const V4 po = sub(cp, p12);
+  const float d2 = dot(po, po);
+  const float L = dot(e, e);
+  {
+    const float Q = dot(po, e);
+    if (d2 >= k.d2_out && d2 < 1e18f && L > 1e-30f && L < 1e18f &&
+        d2 * L - Q * Q > fmaf_(CYL_PRECULL_K, d2, k.r2m_pre) * L)
+      return no_cand();
+  }
+  // cyl_project (rt4_intersect.h): miss on a short in-plane direction, then the normalisation
+  if (length(r1d) < SMALL_F) return no_cand();
+  const float len = sqrt_(L);  // length(e)
+  if (len < SMALL_F) return no_cand();
+  const V4 dn = divs(e, len);
+  const float dp = dot(po, dn);
+  if (sphere_culled(d2, dp, k.d2_out, k.r2m)) return no_cand();
+  Cand c = sphere_cand_d(d2, dp, r, dc, outer, id);
+  c.dist = c.dist / len;  // inter.dist /= drct_in_plane_length (:265)
+  return c;
+}
 #ifndef RT4_CYL_CULL
-#define RT4_CYL_CULL 1  // the sphere cull for the cylinders and the union's cylinders (A/B knob)
+#define RT4_CYL_CULL 1  // the sphere cull for the cylinders and the union's cylinders: 1 after the projection's
+                        // normalisation, 2 also before it (config 5 -0.4 %: few waves cull every lane, and the
+                        // extra test costs more than the divisions it skips; profiles/r05_ab.txt)
 #endif
 #ifndef RT4_TIGER_CULL
 #define RT4_TIGER_CULL 0  // the sphere cull for the tiger's axes pairs and split quarters: config 4 -1.3 %, config 5
@@ -230,14 +260,18 @@ __device__ __forceinline__ Cand union_cand(const rt4_scene_desc* __restrict__ S,
   const V4 p1 = ld4(u.cylinder1.point), a11 = ld4(u.cylinder1.axis1), a12 = ld4(u.cylinder1.axis2);
   const V4 p2 = ld4(u.cylinder2.point), a21 = ld4(u.cylinder2.axis1), a22 = ld4(u.cylinder2.axis2);
   const float gt = X->union_gt[i];
-#if RT4_CYL_CULL
+#if RT4_CYL_CULL == 2
+  Cand c1 = cyl_cand_precull(p1, a11, a12, ray, u.cylinder1.r, X->union_r[i][0], X->union_cull[i][0], true, base);
+#elif RT4_CYL_CULL
   Cand c1 = cyl_cand_cull(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], X->union_cull[i][0], true,
                           base);
 #else
   Cand c1 = cyl_cand(cyl_project(p1, a11, a12, ray), p1, u.cylinder1.r, X->union_r[i][0], true, base);
 #endif
   if (c1.hit && axes_dist_sq(c1.dist, ray, p2, a21, a22) > gt) c1.hit = false;
-#if RT4_CYL_CULL
+#if RT4_CYL_CULL == 2
+  Cand c2 = cyl_cand_precull(p2, a21, a22, ray, u.cylinder2.r, X->union_r[i][1], X->union_cull[i][1], true, base + 1);
+#elif RT4_CYL_CULL
   Cand c2 = cyl_cand_cull(cyl_project(p2, a21, a22, ray), p2, u.cylinder2.r, X->union_r[i][1], X->union_cull[i][1], true,
                           base + 1);
 #else
@@ -652,7 +686,11 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
     for_count<NCY>(S->n_cylinders, [&](int i) {
       const rt4_cylinder& c = S->cylinders[i];
       const V4 cp = ld4(c.point);
-#if RT4_CYL_CULL
+#if RT4_CYL_CULL == 2
+      inter = closest(cyl_cand_precull(cp, ld4(c.axis1), ld4(c.axis2), ray, c.r, X->cyl_r[i], X->cyl_cull[i], true,
+                                       B.cyl + static_cast<uint32_t>(i)),
+                      inter);
+#elif RT4_CYL_CULL
       inter = closest(cyl_cand_cull(cyl_project(cp, ld4(c.axis1), ld4(c.axis2), ray), cp, c.r, X->cyl_r[i], X->cyl_cull[i],
                                     true, B.cyl + static_cast<uint32_t>(i)),
                       inter);

@@ -1870,6 +1870,7 @@ int build_aux(rt4_context* ctx, const rt4_scene_desc& s, SceneAux* a, char* err,
     k->d2_out = std::isnan(r) ? NAN : sqrt_lt_threshold(std::max(r, 0.0003f));
     const bool ok = r >= 1e-15f && r <= 1e15f;  // r <= 0: sin_oap < 1 always, never cull
     k->r2m = ok ? static_cast<float>(static_cast<double>(r) * r * (1.0 + 1e-4)) : INFINITY;
+    k->r2m_pre = ok ? std::nextafter(static_cast<float>(static_cast<double>(k->r2m) * (1.0 + 1e-6)), INFINITY) : INFINITY;
   };
   for (int i = 0; i < s.n_spheres; i++) cull_of(s.spheres[i].r, s.spheres[i].center, &a->sphere_cull[i]);
   for (int i = 0; i < s.n_cylinders; i++) {
