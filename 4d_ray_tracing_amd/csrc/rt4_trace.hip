@@ -115,6 +115,10 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_TIGER_SPLIT
 #define RT4_TIGER_SPLIT 16  // in-wave split of the tiger test in the lockstep kernels: the most lanes split (0 = off)
 #endif
+#ifndef RT4_REFILL_OPEN_TIGER
+#define RT4_REFILL_OPEN_TIGER 2  // the refill threshold of the open tiger kernels (0: REFILL_MIN): config 5 +0.6 % at 2
+                                 // (3: +0.3 %, 4: +0.25 %; r05-v51, profiles/r05_ab.txt)
+#endif
 #ifndef RT4_TIGER_SPLIT_REUSE
 #define RT4_TIGER_SPLIT_REUSE 1  // the split in the lockstep kernels' primary-reuse instantiations too
 #endif
@@ -600,7 +604,8 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
                          !phase_refill_of(K) && sh_count(K, 2) != 0;
   constexpr bool PHASE = phase_refill_of(K);
   constexpr unsigned REFILL_K =
-      K != GENERIC && (K >> 8) != 0 && !(K & K_TIGER) && !PHASE && !REUSE ? static_cast<unsigned>(RT4_REFILL_MIN_OPEN)
+      K != GENERIC && (K >> 8) != 0 && !PHASE && !REUSE && (RT4_REFILL_OPEN_TIGER > 0 || !(K & K_TIGER))
+          ? static_cast<unsigned>((K & K_TIGER) ? RT4_REFILL_OPEN_TIGER : RT4_REFILL_MIN_OPEN)
                                                                           : REFILL_MIN;
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
   // Wave clock (closed scenes): while almost every path of the wave runs all R + 1 bounces
