@@ -129,7 +129,7 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #define RT4_BEAT_SLACK 0  // in-beat tiger deferral in the lockstep kernels: parked iterations per sample (0 = off)
 #endif
 #ifndef RT4_DEFER_TIGER_WAIT
-#define RT4_DEFER_TIGER_WAIT 4
+#define RT4_DEFER_TIGER_WAIT 6  // r05-v52: 6 (config 5 +0.4 % over 4 in 5 rounds; 3 and 12 slower; profiles/r05_ab.txt)
 #endif
 #ifndef RT4_DEFER_EXACT
 // Deferred exact sphere tests: a wave runs its pending exact sphere tests only once at

@@ -244,7 +244,7 @@ def test_config4_pipelined_equals_sequential(rt4):
         (p, np_), (q, nq) = frames_both_ways(rt4, scene, us, reg, 0, rt4.FLAG_SAMPLER_LUT, reserve=True)
         assert np_ == nq
         if identical:
-            assert np_ == 3 * 6898035764  # the config-4 frame's count (profiles/r05_v51/pmc_config4.json bench.intersections_per_step)
+            assert np_ == 3 * 6898035764  # the config-4 frame's count (profiles/r05_v52/pmc_config4.json bench.intersections_per_step)
         assert same_bits(p, q)
 
 
