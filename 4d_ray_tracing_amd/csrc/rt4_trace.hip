@@ -115,6 +115,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_TIGER_SPLIT
 #define RT4_TIGER_SPLIT 16  // in-wave split of the tiger test in the lockstep kernels: the most lanes split (0 = off)
 #endif
+#ifndef RT4_SAVE_HYPER
+#define RT4_SAVE_HYPER 0  // the tiger kernels' register savings (RT4_WAVE_COUNT, RT4_FLUSH_REMAT) in the hypercube kernels
+#endif
 #ifndef RT4_REFILL_OPEN_TIGER
 #define RT4_REFILL_OPEN_TIGER 2  // the refill threshold of the open tiger kernels (0: REFILL_MIN): config 5 +0.6 % at 2
                                  // (3: +0.3 %, 4: +0.25 %; r05-v51, profiles/r05_ab.txt)
@@ -694,7 +697,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   // wave's first thread from a scalar register and the lane from mbcnt where it runs, so no VGPR keeps them (or their
   // LDS addresses) live across the tiger test, the loop's register peak; there they were spilled. The sphere and
   // hypercube kernels measured 1.4 % / 5.7 % slower with it (profiles/r05_ab.txt) and keep the plain form.
-  constexpr bool REMAT = RT4_FLUSH_REMAT && K != GENERIC && (K & K_TIGER);
+  constexpr bool REMAT = RT4_FLUSH_REMAT && K != GENERIC && ((K & K_TIGER) || (RT4_SAVE_HYPER && (K & K_HYPERCUBE)));
   const unsigned wave_s = __builtin_amdgcn_readfirstlane(wbase);
   unsigned in_next = 64;  // wave-uniform: next inbox entry to hand out (64: empty)
   // RT4_CLAIM_TILES > 1: one atomic claims that many consecutive tiles; the spare ones are used in turn.
@@ -713,7 +716,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   // Without primary reuse every counted call is evaluated and a lane adds at most one per iteration: the wave
   // counts them in a wave-uniform (scalar) register from one ballot per iteration instead of a VGPR per lane,
   // which frees a register in the register-bound tiger kernels (RT4_WAVE_COUNT).
-  constexpr bool WAVE_COUNT = RT4_WAVE_COUNT && !REUSE && K != GENERIC && (K & K_TIGER);
+  constexpr bool WAVE_COUNT = RT4_WAVE_COUNT && !REUSE && K != GENERIC && ((K & K_TIGER) || (RT4_SAVE_HYPER && (K & K_HYPERCUBE)));
   unsigned long long w_inter = 0;
 
 #ifdef RT4_LANESTATS
