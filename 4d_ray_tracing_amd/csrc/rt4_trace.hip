@@ -115,6 +115,9 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_TIGER_SPLIT
 #define RT4_TIGER_SPLIT 16  // in-wave split of the tiger test in the lockstep kernels: the most lanes split (0 = off)
 #endif
+#ifndef RT4_REFILL_HYPER
+#define RT4_REFILL_HYPER 0  // the refill threshold of the open hypercube kernels (0: RT4_REFILL_MIN_OPEN; A/B knob)
+#endif
 #ifndef RT4_SAVE_HYPER
 #define RT4_SAVE_HYPER 0  // the tiger kernels' register savings (RT4_WAVE_COUNT, RT4_FLUSH_REMAT) in the hypercube kernels
 #endif
@@ -608,7 +611,9 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   constexpr bool PHASE = phase_refill_of(K);
   constexpr unsigned REFILL_K =
       K != GENERIC && (K >> 8) != 0 && !PHASE && !REUSE && (RT4_REFILL_OPEN_TIGER > 0 || !(K & K_TIGER))
-          ? static_cast<unsigned>((K & K_TIGER) ? RT4_REFILL_OPEN_TIGER : RT4_REFILL_MIN_OPEN)
+          ? static_cast<unsigned>((K & K_TIGER) ? RT4_REFILL_OPEN_TIGER
+                                                : ((K & K_HYPERCUBE) && RT4_REFILL_HYPER > 0 ? RT4_REFILL_HYPER
+                                                                                              : RT4_REFILL_MIN_OPEN))
                                                                           : REFILL_MIN;
   int defer_age = 0;  // wave-uniform: iterations since the wave's parked lanes were first parked
   // Wave clock (closed scenes): while almost every path of the wave runs all R + 1 bounces
