@@ -243,6 +243,50 @@ def test_find_intersection_rays_on_infinite_cylinders(rt4, oracle, name):
     assert_bits(gc, cc, f"{name} on-cylinder material color")
 
 
+def grazing_cylinder_rays(cyls, n_per, seed):
+    """Rays whose projection onto a cylinder's circle plane passes the circle at r (1 + e), |e| from 1e-8 to
+    1e-1 and both signs, from outside, with a random component along the axes: the boundary of the cylinders'
+    sphere cull (rt4_fast.h cyl_cand_cull, rt4_aux.h SphereCull)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for cp, a1, a2, r in cyls:
+        cp, a1, a2 = (np.array(v, np.float64) for v in (cp, a1, a2))
+        for _ in range(n_per):
+            b1, b2 = np.linalg.qr(np.stack([a1, a2] + list(rng.normal(size=(2, 4)))).T)[0].T[2:]
+            th = rng.uniform(0, 2 * np.pi)
+            u = np.cos(th) * b1 + np.sin(th) * b2
+            v = -np.sin(th) * b1 + np.cos(th) * b2
+            L = r * np.exp(rng.uniform(np.log(2.0), np.log(60.0)))
+            e = rng.choice([-1.0, 1.0]) * 10.0 ** rng.uniform(-8, -1) if rng.random() > 1 / 16 else 0.0
+            sa = min(r * (1.0 + e) / L, 1.0)
+            dp = -u * np.sqrt(1.0 - sa * sa) + v * sa
+            d = dp * rng.uniform(0.3, 1.0) + rng.normal(0, 0.5) * a1 + rng.normal(0, 0.5) * a2
+            p = cp + L * u + rng.uniform(-3, 3) * a1 + rng.uniform(-3, 3) * a2
+            out.append(np.concatenate([p, d / np.linalg.norm(d)]))
+    return np.array(out, np.float32)
+
+
+@pytest.mark.parametrize("name", ["cylinder4d", "all_primitives"])
+def test_find_intersection_grazing_cylinders(rt4, oracle, name):
+    """Bit-exact on rays grazing the cylinders and the union's cylinders, where the cull (r05-v50) decides."""
+    d = rt4.Scene.named(name).desc
+    cyls = [(list(c.point), list(c.axis1), list(c.axis2), c.r) for c in (d.cylinders[i] for i in range(d.n_cylinders))]
+    for q in range(d.n_unions):
+        u = d.unions[q]
+        cyls += [(list(c.point), list(c.axis1), list(c.axis2), c.r) for c in (u.cylinder1, u.cylinder2)]
+    assert cyls
+    rays = grazing_cylinder_rays(cyls, 8000, 321)
+    c, cc = oracle.find_intersection(d, rays)
+    t = rt4.Tracer(device=0, scene=rt4.Scene(d))
+    try:
+        g, gc = t.debug_find_intersection(rays)
+    finally:
+        t.close()
+    assert_bits(g, c, f"{name} grazing-cylinder find_intersection")
+    assert_bits(gc, cc, f"{name} grazing-cylinder material color")
+    assert (c[:, 0] > 0).mean() > 0.05
+
+
 # -------------------------------------------------------------------------------------- images
 def render_both(rt4, oracle, scene, u, reg, flags=0, old=None):
     t = rt4.Tracer(device=0, flags=flags, scene=scene)
