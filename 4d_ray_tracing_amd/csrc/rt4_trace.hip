@@ -28,6 +28,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <chrono>
@@ -136,6 +137,15 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #endif
 #ifndef RT4_DEFER_TIGER_WAIT
 #define RT4_DEFER_TIGER_WAIT 6  // r05-v52: 6 (config 5 +0.4 % over 4 in 5 rounds; 3 and 12 slower; profiles/r05_ab.txt)
+#endif
+#ifndef RT4_DEFER_EXACT_TIGER
+// Deferred exact sphere tests in the open tiger kernels (round 6; rt4_trace_kernel SDEFER): the
+// wave's pending-lane threshold (0 = off) and the most iterations a lane waits. A lane whose sphere cull leaves
+// pending spheres parks before any other group and redoes the cull next iteration (no state kept), as in §4.25.
+#define RT4_DEFER_EXACT_TIGER 0
+#endif
+#ifndef RT4_DEFER_WAIT_TIGER
+#define RT4_DEFER_WAIT_TIGER 4
 #endif
 #ifndef RT4_DEFER_EXACT
 // Deferred exact sphere tests: a wave runs its pending exact sphere tests only once at
@@ -634,6 +644,12 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   constexpr int BEAT_SLACK = PHASE && CLOCK ? RT4_BEAT_SLACK : 0;
   constexpr bool TDEFER = RT4_DEFER_TIGER > 0 && !REUSE && K != GENERIC && (K & K_TIGER) && (!PHASE || BEAT_SLACK > 0);
   int slack = BEAT_SLACK;            // BEAT_SLACK: the lane's parked iterations left in this sample
+  // Deferred exact sphere tests next to the deferred tiger (RT4_DEFER_EXACT_TIGER > 0): the open tiger kernels with
+  // spheres (all_primitives, BASELINE config 5) split find_cand<K, false> into find_pre (spaces + sphere cull), the
+  // pending exact tests and find_rest without the tiger, the same ops in the same order; a lane with pending spheres
+  // parks until RT4_DEFER_EXACT_TIGER lanes of the wave have some, or RT4_DEFER_WAIT_TIGER iterations (defer_age).
+  constexpr bool SDEFER = RT4_DEFER_EXACT_TIGER > 0 && RT4_SPHERE_CULL && TDEFER && !PHASE && !REUSE && K != GENERIC &&
+                          (K & K_SPHERES) && sh_count(K, 2) != 0;
   // In-wave split of the tiger test (RT4_TIGER_SPLIT = the most lanes split, 0 = off): when at
   // most that many lanes of the wave need the tiger test in an iteration, each one's test is cut into its four
   // (axes pair, radius) quarters (rt4_fast.h tiger_quarter), run on four lanes at once through a per-wave LDS
@@ -1043,6 +1059,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
       Cand pre = no_cand();
       bool need = false;
       const bool held = CLOCK && parked;  // held for the wave clock (the lockstep kernels)
+      bool fresh = false;                 // SDEFER: the lane starts a find this iteration
       if (active && !held) {
         if constexpr (CLOCK && REUSE) {  // as the generic path below: bounce 0 from the cache at the clock boundary
           cached = use_cached;
@@ -1053,8 +1070,33 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         } else if (tparked) {
           pre = unpack_cand(cold[512]);
           need = true;
+        } else if constexpr (SDEFER) {
+          fresh = true;
         } else {
           pre = find_cand<K, false>(S, X, P, ray);  // every group but the tiger, in order
+          need = !(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray));
+        }
+      }
+      if constexpr (SDEFER) {
+        // find_cand<K, false> in its three parts, the pending exact sphere tests deferred (the same bits)
+        uint32_t pend = 0;
+        SphereGeo geo;
+        Cand inter = no_cand();
+        if (fresh) inter = find_pre<K>(S, X, ray, pend, nullptr);
+        const unsigned long long pm = __ballot(pend != 0u);
+        const bool run = pm != 0ull && (static_cast<unsigned>(__popcll(pm)) >= static_cast<unsigned>(RT4_DEFER_EXACT_TIGER) ||
+                                        defer_age >= RT4_DEFER_WAIT_TIGER || pm == __ballot(fresh));
+        if (pm != 0ull && !run) {
+          if (pend != 0u) {
+            parked = true;
+            fresh = false;
+          }
+          ++defer_age;
+        } else {
+          defer_age = 0;
+        }
+        if (fresh) {
+          pre = find_rest<K, false>(S, X, P, ray, exact_pending<K, false>(X, P, ray, geo, pend, inter));
           need = !(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray));
         }
       }
@@ -1080,8 +1122,9 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         const unsigned long long tm = __ballot(need);
         // in-beat: a lane with no parked iteration left forces the run (its sample must end within the period)
         const bool forced = BEAT_SLACK > 0 && clock_on() && __ballot(need && slack <= 0) != 0ull;
+        // (!parked: as !held, and it leaves out the lanes parked for their exact sphere tests, SDEFER)
         const bool run = tm != 0ull && (static_cast<unsigned>(__popcll(tm)) >= static_cast<unsigned>(RT4_DEFER_TIGER) ||
-                                        tdefer_age >= RT4_DEFER_TIGER_WAIT || tm == __ballot(active && !held) || forced);
+                                        tdefer_age >= RT4_DEFER_TIGER_WAIT || tm == __ballot(active && !parked) || forced);
         if (tm != 0ull && !run) {
           ++tdefer_age;
           if (need) {
@@ -1158,11 +1201,15 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
             tray[2u * rk] = make_float4(ray.point.x, ray.point.y, ray.point.z, ray.point.w);
             tray[2u * rk + 1u] = make_float4(ray.drct.x, ray.drct.y, ray.drct.z, ray.drct.w);
           }
+          // Cross-lane hand-offs through LDS: a wave's LDS accesses complete in program order, and the wave barrier
+          // keeps the compiler from moving one lane's read of another lane's slot above the write.
+          __builtin_amdgcn_wave_barrier();
           if (ln < 4u * ng) {  // quarter ln & 3 of the test of the lane ranked ln >> 2
             const float4 p4 = tray[2u * (ln >> 2)], d4 = tray[2u * (ln >> 2) + 1u];
             tres[ln] = pack_cand(tiger_quarter(S, X, 0, prim_bases<K>(X).tiger,
                                                Ray{V4{p4.x, p4.y, p4.z, p4.w}, V4{d4.x, d4.y, d4.z, d4.w}}, ln & 3u));
           }
+          __builtin_amdgcn_wave_barrier();
           if (go)
             tg = closest(closest(unpack_cand(tres[4u * rk]), unpack_cand(tres[4u * rk + 1u])),
                          closest(unpack_cand(tres[4u * rk + 2u]), unpack_cand(tres[4u * rk + 3u])));
@@ -2148,7 +2195,17 @@ int rt4_context_create(int device, uint32_t flags, rt4_context** out, char* err,
     if (e == hipSuccess) e = hipDeviceSynchronize();
   }
   if (e == hipSuccess && (flags & RT4_FLAG_SAMPLER_LUT)) {
-    e = hipMalloc(&c->d_wlut, (sizeof(WEntry) << 23) * RT4_ABL_WLUT_STRIDE);
+    // Diagnostic (round 6): RT4_WLUT_ALLOC=fine|uncached places the table in fine-grained or
+    // uncached device memory, to measure whether a 4-B gather then leaves L2 as a smaller fabric request. The
+    // default (coarse-grained hipMalloc) is what every product launch uses; images do not depend on it.
+    const char* wa = std::getenv("RT4_WLUT_ALLOC");
+    unsigned wflags = !wa ? hipDeviceMallocDefault
+                          : !std::strcmp(wa, "fine")     ? hipDeviceMallocFinegrained
+                          : !std::strcmp(wa, "uncached") ? hipDeviceMallocUncached
+                                                         : hipDeviceMallocDefault;
+    e = wflags == hipDeviceMallocDefault
+            ? hipMalloc(&c->d_wlut, (sizeof(WEntry) << 23) * RT4_ABL_WLUT_STRIDE)
+            : hipExtMallocWithFlags(reinterpret_cast<void**>(&c->d_wlut),(sizeof(WEntry) << 23) * RT4_ABL_WLUT_STRIDE, wflags);
     if (e == hipSuccess) {
       hipLaunchKernelGGL(rt4_build_wlut_kernel, dim3((1u << 23) / 256), dim3(256), 0, 0, c->d_wlut);
       e = hipGetLastError();
@@ -2510,6 +2567,10 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
       // scene, the slot buffer and the queue words stay valid), then clear the count it left in its slot
       (void)hipStreamSynchronize(ts);
       (void)hipMemsetAsync(count, 0, sizeof(unsigned long long), s);
+      // the launch that reuses this count slot waits on seq_done[slot]: record it (and done) again behind the
+      // memset, so that launch's trace cannot add to the slot before it is cleared
+      (void)hipEventRecord(ctx->seq_done[slot], s);
+      (void)hipEventRecord(ctx->done, s);
     }
     rt4_set_err(err, errlen, "trace kernel launch failed: %s", hipGetErrorString(le));
     return RT4_ERR_HIP;

@@ -169,14 +169,17 @@ def report_failure(rank: int, msg: str) -> None:
             pass
 
 
-def failure() -> str | None:
-    """The failure a rank reported, or None."""
+def failure(unreachable_is_failure: bool = False) -> str | None:
+    """The failure a rank reported, or None. With unreachable_is_failure, a store that no longer answers is reported
+    as a failure too: when the rank that hosts the store (rank 0 under plain env:// init, without torchrun's agent)
+    has exited after a failure, its peers' gathers never complete and nothing else would end their wait."""
     st = _store()
     try:
         if st is not None and st.check([FAIL_KEY]):
             return st.get(FAIL_KEY).decode()
-    except Exception:
-        pass
+    except Exception as e:
+        if unreachable_is_failure:
+            return f"store unreachable ({type(e).__name__}: {e})"
     return None
 
 
@@ -195,7 +198,7 @@ def wait_or_failure(stream=None, check_s: float = 0.01) -> str | None:
     while not ev.query():
         now = time.perf_counter()
         if now >= next_check:
-            f = failure()
+            f = failure(unreachable_is_failure=True)
             if f is not None:
                 return f
             next_check = now + check_s

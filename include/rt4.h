@@ -382,8 +382,9 @@ typedef struct rt4_region {
  * (one per ray-bounce, shader.frag:475). stream: hipStream_t (NULL = default stream).
  * Asynchronous: no host synchronisation and no allocation once the context's buffers hold the launch: the
  * tile-order buffer covers 2^18 8x8 tiles (16.7 M pixels; a larger launch grows it once) and the overlap's slot
- * buffers grow to the largest frame seen (RT4_FLAG_SERIAL_FRAMES: the first launch of a larger frame waits for
- * the launches in flight and allocates; rt4_context_reserve_overlap does it ahead of time). Launches of one
+ * buffers grow to the largest frame seen (without RT4_FLAG_SERIAL_FRAMES, the default: the first launch of a larger
+ * frame waits for the launches in flight and allocates; rt4_context_reserve_overlap does it ahead of time; a
+ * serial context has no slot buffers). Launches of one
  * context run in submission order: a launch on another stream than the previous one waits for it. */
 int rt4_render_device(rt4_context* ctx, const rt4_uniforms* u, const rt4_region* region, float* d_rgba,
                       int64_t row_stride_px, unsigned long long* d_counter, void* stream, char* err,
@@ -486,7 +487,8 @@ int rt4_bands_unpermute_device(const void* d_gathered, void* d_image, int32_t wi
 /* Bytes of the context's frame-colour scratch for pipelined frames (0 before any pipelined launch or
  * reservation; a scene that runs frame by frame never allocates it). */
 uint64_t rt4_context_frame_scratch_bytes(const rt4_context* ctx);
-/* Bytes of the context's overlap slot buffers (RT4_FLAG_SERIAL_FRAMES: 0 before any single-frame launch). */
+/* Bytes of the context's overlap slot buffers (without RT4_FLAG_SERIAL_FRAMES, the default: 0 before any single-frame
+ * launch or reservation; a context made with RT4_FLAG_SERIAL_FRAMES always returns 0). */
 uint64_t rt4_context_overlap_bytes(const rt4_context* ctx);
 /* Allocates the slot buffers that overlapped single-frame launches of one w x h image use with the context's
  * current scene (3, or 8 for a frame too small to fill the chip), so that the first such launch neither

@@ -232,6 +232,28 @@ def test_cpp_host_bands_failed_gather_aborts_cleanly(rt4, tmp_path, gpus, rehear
     assert not os.path.exists(pre + "_yxz.ppm")
 
 
+@pytest.mark.parametrize("gpus,fail", [(2, 1), (8, 5)])
+def test_cpp_host_bands_failed_gather_aborts_real_peers(rt4, tmp_path, gpus, fail):
+    """the failed-gather path with real peers. Rank `fail` (not the root) skips its ncclGather while the
+    other ranks' gathers are enqueued on communicators made by ncclCommInitAll; every rank must abort its
+    communicator (ncclCommAbort from its own host thread), which has to release the peers already waiting in the
+    gather, and the program exits with status 1 naming the rank. Needs as many devices as ranks: skipped on the
+    one-GPU test box, so this path is unverified on hardware until a multi-GPU box runs it."""
+    import os
+
+    import torch
+
+    if torch.cuda.device_count() < gpus:
+        pytest.skip(f"needs {gpus} devices, the box has {torch.cuda.device_count()}")
+    pre = str(tmp_path / "g")
+    r = _run_render(rt4, ["-p", _props_with(tmp_path, 2, 2), "-s", "sphere", "-n", "3", "-W", "160", "-H", "90",
+                          "--gpus", str(gpus), "-o", pre],
+                    env={"RT4_RENDER_FAIL_RANK": str(fail), "RT4_RENDER_FAIL_STAGE": "gather"})
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert f"rank {fail}: " in r.stderr and "failure injected (RT4_RENDER_FAIL_STAGE=gather)" in r.stderr, r.stderr
+    assert not os.path.exists(pre + "_yxz.ppm")
+
+
 def test_reserve_frames_sizes_one_chunk(rt4):
     """rt4_context_reserve_frames allocates nothing for a region that runs frame by frame (wider than the
     pipelined pixel word holds), and exactly one chunk of frames otherwise: config 4's 4K

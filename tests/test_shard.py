@@ -217,3 +217,29 @@ def test_gather_failure_on_one_rank_ends_every_rank(tmp_path, world):
     for r in range(world):
         text = (tmp_path / f"rank{r}.log").read_text()
         assert "rank 1: GatherError: gather failure injected" in text, (r, text)
+
+
+def test_unreachable_store_ends_the_wait(monkeypatch):
+    """when the rank that hosts the store has exited after a failure, a peer's gather never completes and
+    its store reads raise. wait_or_failure must then report a failure ('store unreachable') instead of polling
+    forever; a plain failure() call (report paths) still returns None."""
+    shard = importlib.import_module("4d_ray_tracing_amd.shard")
+
+    class GoneStore:
+        def check(self, keys):
+            raise RuntimeError("Connection reset by peer")
+
+    monkeypatch.setattr(shard, "_store", lambda: GoneStore())
+    assert shard.failure() is None
+    msg = shard.failure(unreachable_is_failure=True)
+    assert msg is not None and msg.startswith("store unreachable") and "Connection reset" in msg
+
+    class Pending:  # a device event that never completes (the gather the dead rank never joins)
+        def record(self, stream=None):
+            pass
+
+        def query(self):
+            return False
+
+    monkeypatch.setattr(torch.cuda, "Event", Pending)
+    assert shard.wait_or_failure(check_s=0.001).startswith("store unreachable")
