@@ -94,6 +94,7 @@ def parse_args(argv=None):
     p.add_argument("--no-reuse-leg", action="store_true", help="skip the extra primary-reuse leg (N = 1)")
     p.add_argument("--no-fbf-leg", action="store_true", help="skip the extra frame-by-frame leg (N = 1)")
     p.add_argument("--no-sections-leg", action="store_true", help="skip the extra 4D-view frame-loop leg (N = 1)")
+    p.add_argument("--no-steady-leg", action="store_true", help="skip the extra sustained-clock leg (N = 1)")
     p.add_argument("--hw-queues", type=int, default=8,
                    help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's)")
     p.add_argument("--frame-by-frame", action="store_true",
@@ -224,7 +225,8 @@ def pmc_profile(config, frames_per_dispatch):
     workload, kernel version and launch shape (frames per pipelined dispatch) as this run, or None."""
     keys = ("scene", "width", "height_per_gpu", "spp", "bounces", "seed", "sampler_lut", "frame_format",
             "kernel_version", "progressive")
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_*.json"), recursive=True)):
+    # the newest round's profile first (profiles/r06_v52 before profiles/r05_v52); only the per-config summaries
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_config*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
@@ -583,6 +585,36 @@ def main():
             "intersections_per_step": n_r / args.steps, "evaluated_per_step": t_r.evaluated() / args.steps,
         }
         t_r.close()
+    # Extra leg (N = 1, pipelined): the headline's frames at the clock the chip holds under sustained load. The timed
+    # frames above follow only `warmup` frames (the driver's 5: ~2 ms of work after idle), and the chip's clock is still
+    # ramping through them: 2.0-2.2 GHz on config 2, against 2.35 after ~60 ms of load (tools/clock_probe.sh,
+    # profiles/r06/clock). Here the same frames run two full launches to load the chip, then two more are timed.
+    # Reported beside the headline, never as value.
+    steady_leg = None
+    if world == 1 and pipelined and not args.no_steady_leg:
+        # two launches' worth of frames, fewer for long frames (>= 150 ms of load either way; a 4K frame of config 4 is
+        # ~70 ms, already at a sustained clock)
+        fpl_s = tracer.frames_per_launch(reg.w, reg.h)
+        n_st = max(2, min(2 * fpl_s, int(150.0 / max(kernel_ms, 1e-3))))
+        frame_no[0] = 0
+        frame.zero_()
+        render_frames(n_st, 0)
+        cnt_s = torch.zeros(1, dtype=torch.int64, device=dev)
+        es0 = torch.cuda.Event(enable_timing=True)
+        es1 = torch.cuda.Event(enable_timing=True)
+        es0.record(stream)
+        render_frames(n_st, cnt_s.data_ptr())
+        es1.record(stream)
+        torch.cuda.synchronize()
+        n_s = int(cnt_s.item())
+        ms_s = es0.elapsed_time(es1) / n_st
+        steady_leg = {
+            "label": "sustained clock: the same frames, timed after as many frames of load (the headline's timed "
+                     "frames run while the clock ramps from idle; DESIGN.md section 9); never the value",
+            "frames": n_st, "frames_before": n_st, "frames_per_launch": min(n_st, fpl_s),
+            "value": n_s / (ms_s * 1e-3) / n_st, "unit": "ray-bounce intersections/s",
+            "kernel_ms": ms_s, "intersections_per_step": n_s / n_st,
+        }
     sections_leg = None
     if world == 1 and not args.no_sections_leg:
         sections_leg = sections_loop_leg(rt4, torch, gpu, flags, scene, stream, tracer)
@@ -657,6 +689,8 @@ def main():
             line["frame_by_frame_leg"] = fbf_leg
         if sections_leg:
             line["sections_loop_leg"] = sections_leg
+        if steady_leg:
+            line["steady_clock_leg"] = steady_leg
         if strong:
             line["t1_ms"] = t1_ms if world > 1 else ms_per_step
             line["efficiency"] = (line["t1_ms"] / (world * ms_per_step)) if line["t1_ms"] else None
@@ -680,12 +714,17 @@ def main():
                                  "x units / kernel time; counts work the kernel skips exactly (tiger CSE, "
                                  "bounding-ball skips, the sampler table), so it is not a hardware utilisation",
                 "ops_per_unit": opu,
-                "ops_per_unit_executed": opu if args.no_lut else opu_exec,
-                "frac_executed": achieved_exec / PEAK_FP32_VALU_TFLOPS,
+                "frac_reference": achieved / PEAK_FP32_VALU_TFLOPS,
+                # the reference's count without the Newton loop the sampler table replaces (round 1-5's "executed")
+                "ops_per_unit_reference_lut": opu if args.no_lut else opu_exec,
+                "frac_reference_lut": achieved_exec / PEAK_FP32_VALU_TFLOPS,
+                "frac_executed": None,  # from the PMC profile's FLOP counters, below
                 "units_per_launch": units_per_launch,
                 "algorithmic_bytes_per_launch": reg.w * reg.h * 2 * rt4.frame_format_bytes(fmt),  # old_frame in, new out
                 "note": "fp32 ops (fma=2) per find_intersection+shading counted by the oracle on a row sample of "
-                        "the frame; executed = without the w_by_volume Newton ops the sampler table replaces; "
+                        "the frame (frac = frac_reference); reference_lut = without the w_by_volume Newton ops the "
+                        "sampler table replaces; frac_executed = the fp32 FLOPs the kernel executed (hardware FLOP "
+                        "counter x lane utilisation, DESIGN.md §5) / kernel time / peak; "
                         "per launch = per frame (a pipelined launch holds frames_per_launch frames: its units, "
                         "bytes and time are divided by them); frac_counters = the VALU lane-operations the "
                         "hardware counted (SQ_THREAD_CYCLES_VALU, same config, kernel version and launch shape) / "
@@ -697,6 +736,19 @@ def main():
                 line["roofline"]["valu_lane_ops_per_frame"] = lane_ops
                 line["roofline"]["valu_lane_utilisation"] = der.get("valu_lane_utilisation")
                 line["roofline"]["valu_issue_frac"] = der.get("valu_issue_frac")
+                if cnt.get("SQ_INSTS_VALU_FLOPS_FP32") and cnt.get("SQ_INSTS_VALU"):
+                    # SQ_INSTS_VALU_FLOPS_FP32 counts a wave instruction's FLOPs once whatever its EXEC mask (fma = 2,
+                    # add / mul / transcendental = 1); SQ_THREAD_CYCLES_VALU counts active lanes, a transcendental
+                    # twice (tools/flops_calib.hip, profiles/r06/flops_calib.txt). Executed FLOPs = 64 x FLOPS_FP32 x
+                    # the lane utilisation, the fp32 instructions taken at the kernel's mean utilisation.
+                    util_c = lane_ops / (64.0 * (cnt["SQ_INSTS_VALU"] + cnt.get("SQ_INSTS_VALU_TRANS_F32", 0.0)))
+                    flops = 64.0 * cnt["SQ_INSTS_VALU_FLOPS_FP32"] * util_c
+                    line["roofline"]["frac_executed"] = flops / (kernel_ms * 1e-3) / (PEAK_FP32_VALU_TFLOPS * 1e12)
+                    line["roofline"]["flops_executed_per_frame"] = flops
+                    line["roofline"]["fp32_flops_per_valu_inst"] = cnt["SQ_INSTS_VALU_FLOPS_FP32"] / cnt["SQ_INSTS_VALU"]
+                    line["roofline"]["frac_executed_kind"] = (
+                        "fp32 FLOPs executed (SQ_INSTS_VALU_FLOPS_FP32 x 64 x lane utilisation, fma = 2) / kernel time / "
+                        "157.3 TFLOP/s; = frac_counters x FLOPs per VALU instruction / 2")
                 line["roofline"]["counters_source"] = src + (
                     f" (rocprofv3 PMC, {prof.get('frames_per_dispatch', 1)} frames per dispatch, per frame; trace "
                     f"{prof.get('avg_ns', 0) * 1e-6:.4f} ms per frame)")

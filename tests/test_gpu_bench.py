@@ -32,7 +32,10 @@ def test_bench_json_line():
     assert d["value"] > 1e9 and d["value_per_gpu"] == d["value"]
     rf = d["roofline"]
     assert 0 < rf["frac"] < 1 and rf["peak"] == 157.3 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"])
-    assert rf["ops_per_unit_executed"] < rf["ops_per_unit"] and rf["frac_executed"] < rf["frac"]
+    assert rf["ops_per_unit_reference_lut"] < rf["ops_per_unit"] and rf["frac_reference_lut"] < rf["frac"]
+    assert rf["frac_reference"] == rf["frac"]
+    if rf.get("frac_counters") and rf["frac_executed"] is not None:  # a profile of this shape with the FLOP pass
+        assert 0 < rf["frac_executed"] < rf["frac_counters"] < 1
     assert d["setup_ms"]["set_scene_repeat_ms"] < d["setup_ms"]["set_scene_ms"] + 1.0
     # the 4D view's frame loop at properties.txt's sizes: overlapped launches against serial ones (bench.py
     # refuses to print a line when their images or counts differ); the speed-up is reported, not asserted
@@ -40,6 +43,9 @@ def test_bench_json_line():
     sl = d["sections_loop_leg"]
     assert sl["overlapped"]["intersections_per_frame"] == sl["serial"]["intersections_per_frame"] > 0
     assert sl["speedup"] > 0
+    # the sustained-clock leg: the same frames after as many frames of load (never the value)
+    st = d["steady_clock_leg"]
+    assert st["intersections_per_step"] == d["intersections_per_step"] and st["frames"] >= 2 and st["value"] > 1e9
 
 
 def test_bench_strong_config4_one_gpu():

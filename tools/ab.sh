@@ -18,7 +18,7 @@
 set -u -o pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 VDIR=$ROOT/4d_ray_tracing_amd/lib/variants
-COMMON="--no-cpu-baseline --no-ops --no-reuse-leg --no-fbf-leg --no-sections-leg"
+COMMON="--no-cpu-baseline --no-ops --no-reuse-leg --no-fbf-leg --no-sections-leg --no-steady-leg"
 export PYTHONUNBUFFERED=1
 
 steps_of() {  # the bench shape per BASELINE config: as many warmup frames as timed ones (clock ramp)

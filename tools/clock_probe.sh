@@ -21,7 +21,7 @@ OUT=$ROOT/gpurun_out/clock_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 PY=$(command -v python3)
-BASE="--config 2 --no-cpu-baseline --no-ops --no-reuse-leg --no-fbf-leg --no-sections-leg $EXTRA"
+BASE="--config 2 --no-cpu-baseline --no-ops --no-reuse-leg --no-fbf-leg --no-sections-leg --no-steady-leg $EXTRA"
 for place in "${PLACES[@]}"; do
   if [ "$place" = default ]; then unset RT4_WLUT_ALLOC; else export RT4_WLUT_ALLOC=$place; fi
   for shape in "20 20" "128 20"; do

@@ -34,4 +34,8 @@ run pmc_tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_
 run pmc_lat --kernel-trace --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum || true
 # request sizes of the fabric reads (FETCH_SIZE = 128 B x bubble + 64 B x the rest + 32 B x 32B requests)
 run pmc_req --kernel-trace --pmc TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_sum || true
+# fp32 operations the kernel executed (round 6): the FLOP counters (calibrated on gfx950 by
+# tools/flops_calib.hip: EXEC-masked lane counts or wave counts x 64, profiles/r06/flops_calib.txt) and the
+# instruction mix
+run pmc_flops --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU || true
 echo "profile $TAG done"

@@ -13,7 +13,7 @@ for c in $CONFIGS; do
     *) steps="--steps 20 --warmup 20" ;;
   esac
   bash "$ROOT/tools/profile.sh" "${TAG}_config$c" --config "$c" $steps --no-cpu-baseline --no-ops --no-reuse-leg \
-    --no-fbf-leg --no-sections-leg || exit 1
+    --no-fbf-leg --no-sections-leg --no-steady-leg || exit 1
   python3 "$ROOT/tools/pmc_summary.py" "$ROOT/gpurun_out/prof_${TAG}_config$c" > /dev/null || exit 1
   echo "config $c profiled"
 done
