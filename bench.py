@@ -590,12 +590,13 @@ def main():
     # ramping through them: 2.0-2.2 GHz on config 2, against 2.35 after ~60 ms of load (tools/clock_probe.sh,
     # profiles/r06/clock). Here the same frames run two full launches to load the chip, then two more are timed.
     # Reported beside the headline, never as value.
+    # Only where the timed frames are short (< 150 ms in all: configs 2 and 3); longer timed regions (configs 4, 5) run
+    # past the ramp already. Two launches' worth of frames (at least the timed frames, so no launch drains more often
+    # than the headline's), fewer when 150 ms of load takes fewer.
     steady_leg = None
-    if world == 1 and pipelined and not args.no_steady_leg:
-        # two launches' worth of frames, fewer for long frames (>= 150 ms of load either way; a 4K frame of config 4 is
-        # ~70 ms, already at a sustained clock)
+    if world == 1 and pipelined and not args.no_steady_leg and kernel_ms * args.steps < 150.0:
         fpl_s = tracer.frames_per_launch(reg.w, reg.h)
-        n_st = max(2, min(2 * fpl_s, int(150.0 / max(kernel_ms, 1e-3))))
+        n_st = max(args.steps, min(2 * fpl_s, int(150.0 / max(kernel_ms, 1e-3))))
         frame_no[0] = 0
         frame.zero_()
         render_frames(n_st, 0)

@@ -93,6 +93,10 @@ def test_committed_profiles_cover_every_config_of_the_current_kernel(rt4):
         prof = next((p for p in found if p), None)
         assert prof and prof["derived"].get("hbm_bytes_per_launch", 0) > 0, (cfg, version)
         assert prof["counters"].get("SQ_THREAD_CYCLES_VALU", 0) > 0, (cfg, version)
+        # the FLOP pass behind roofline.frac_executed (round 6): executed fp32 FLOPs below the lane-ops
+        c = prof["counters"]
+        assert c.get("SQ_INSTS_VALU_FLOPS_FP32", 0) > 0, (cfg, version)
+        assert 0 < c["SQ_INSTS_VALU_FLOPS_FP32"] < 2 * c["SQ_INSTS_VALU"], (cfg, version)
 
 
 def test_gather_ceiling_is_the_committed_probe():
