@@ -92,6 +92,13 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_ORDER_PREPASS
 #define RT4_ORDER_PREPASS 1  // longest-first tile order from a primary-ray pre-pass (rt4_tile_order_kernel)
 #endif
+#ifndef RT4_LAST_FRAME_ORDER
+// The tile order of a pipelined launch's last frame (round 6, A/B knob): 0 = row-major like the other frames; 1 = its
+// rows in reverse (bottom-up: in the reference's scenes the sky is at the top, so the cheapest tiles go last); 2 = the
+// pre-pass's hit-first order (§4.15) for the last frame only. Only the launch's drain depends on the last frame's
+// order; images and counts do not.
+#define RT4_LAST_FRAME_ORDER 0
+#endif
 #ifndef RT4_SKY_PRETEST
 #define RT4_SKY_PRETEST 1
 #endif
@@ -829,7 +836,9 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
       pos -= frame * a.frame_tiles;
       in_seed = static_cast<uint32_t>(a.frame_seed[frame]);
     }
-    const unsigned btile = order ? order[pos] : pos;
+    const bool last = a.n_frames <= 1 || frame + 1u == static_cast<unsigned>(a.n_frames);  // wave-uniform
+    if (RT4_LAST_FRAME_ORDER == 1 && a.n_frames > 1 && last && a.n_jobs == 1) pos = a.frame_tiles - 1u - pos;
+    const unsigned btile = order && (RT4_LAST_FRAME_ORDER != 2 || last) ? order[pos] : pos;
     const int job = (a.n_jobs > 1 && btile >= a.jobs[1].tile_base) + (a.n_jobs > 2 && btile >= a.jobs[2].tile_base);
     const JobArgs& J = a.jobs[job];
     const unsigned tile = btile - J.tile_base;
@@ -2493,7 +2502,7 @@ int launch_jobs(rt4_context* ctx, const rt4_section_job* jobs, int32_t n_jobs, i
   // Pipelined frames keep row-major order: the longest-first order only shortens the drain at the end
   // of a launch, which a pipelined launch pays once, and in the main phase row-major measured faster
   // (config 2 +1.5 %, config 3 +2 %; profiles/r02_ab.txt).
-  if (!frames && !overlap) {
+  if ((!frames || RT4_LAST_FRAME_ORDER == 2) && !overlap) {
   if (ctx->order_cap < tiles) {  // a frame larger than any before: grow once (allocates)
     HIP_TRY(hipStreamSynchronize(s));
     if (ctx->d_order) (void)hipFree(ctx->d_order);
