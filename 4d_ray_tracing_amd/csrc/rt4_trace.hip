@@ -136,6 +136,16 @@ __device__ __forceinline__ float went_w(WEntry e) { return e; }
 #ifndef RT4_TIGER_SPLIT_REUSE
 #define RT4_TIGER_SPLIT_REUSE 1  // the split in the lockstep kernels' primary-reuse instantiations too
 #endif
+#ifndef RT4_TIGER_SPLIT_OPEN_LDS
+// round 6 (A/B knob): the open tiger kernels split through the mirror room's LDS hand-off after the deferral decides
+// to run (at most RT4_TIGER_SPLIT_OPEN lanes split, more run the direct test) instead of serving over ds_bpermute
+#define RT4_TIGER_SPLIT_OPEN_LDS 0
+#endif
+#ifndef RT4_TIGER_SPLIT_BPERM_RES
+// round 6 (A/B knob): the split's quarter results go back to their owners by ds_bpermute instead of the per-wave LDS
+// area (no lds_tres), so the open kernels' split fits the all_primitives kernel's LDS at 6 blocks per CU
+#define RT4_TIGER_SPLIT_BPERM_RES 0
+#endif
 #ifndef RT4_TIGER_SPLIT_OPEN
 #define RT4_TIGER_SPLIT_OPEN 0  // the same in the open tiger kernels (tiger, all_primitives)
 #endif
@@ -671,10 +681,11 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
   // ds_bpermute (no LDS buffer: the all_primitives kernel's LDS allows no more at 6 blocks per CU). Bit-exact
   // (tools/variant_probe.py) but rejected (profiles/r05_ab.txt, r05-v48 trial): the per-lane pair geometry takes
   // ~40 VGPRs, so the kernel spills at 6 waves and runs 5 (-6.9 % config 5, 20 B spill) or 4 (-12 %, no spill).
-  constexpr bool TSERVE = TSPLIT && TDEFER && !PHASE;
+  constexpr bool TSERVE = TSPLIT && TDEFER && !PHASE && !RT4_TIGER_SPLIT_OPEN_LDS;
   static_assert(!TSPLIT || TSPLIT_MAX <= 16, "one pass of four quarters per test");
-  __shared__ float4 lds_tray[TSPLIT && !TSERVE ? 4 * 32 : 1];  // per wave: up to 16 rays as {point, drct}
-  __shared__ float4 lds_tres[TSPLIT && !TSERVE ? 4 * 64 : 1];  // per wave: 64 quarter results (pack_cand)
+  constexpr bool TRES_LDS = TSPLIT && !TSERVE && !(RT4_TIGER_SPLIT_BPERM_RES && !PHASE);
+  __shared__ float4 lds_tray[TSPLIT && !TSERVE ? 4 * 2 * TSPLIT_MAX : 1];  // per wave: up to TSPLIT_MAX rays {point, drct}
+  __shared__ float4 lds_tres[TRES_LDS ? 4 * 4 * TSPLIT_MAX : 1];  // per wave: 4 quarter results per test (pack_cand)
   __shared__ uint32_t lds_town[TSERVE ? 4 * 16 : 1];            // per wave: the lane of each served test
   bool tparked = false;              // TDEFER: the lane waits for the tiger test with its candidate in cold[512]
   int tdefer_age = 0;                // TDEFER, wave-uniform
@@ -1202,8 +1213,8 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
           // the lanes running the test publish their rays, 4 ng lanes run the quarters, the owners fold their four
           // results (one pass: TSPLIT_MAX <= 16; a loop of passes kept tg live across the quarter and spilled)
           const unsigned ln = rt4_lane_id(), wv = wave_s >> 6;
-          float4* const tray = lds_tray + wv * 32u;
-          float4* const tres = lds_tres + wv * 64u;
+          float4* const tray = lds_tray + wv * (2u * TSPLIT_MAX);
+          float4* const tres = lds_tres + (TRES_LDS ? wv * (4u * TSPLIT_MAX) : 0u);
           const unsigned rk = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(gm >> 32),
                                                         __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(gm), 0u));
           if (go) {
@@ -1213,15 +1224,35 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
           // Cross-lane hand-offs through LDS: a wave's LDS accesses complete in program order, and the wave barrier
           // keeps the compiler from moving one lane's read of another lane's slot above the write.
           __builtin_amdgcn_wave_barrier();
-          if (ln < 4u * ng) {  // quarter ln & 3 of the test of the lane ranked ln >> 2
-            const float4 p4 = tray[2u * (ln >> 2)], d4 = tray[2u * (ln >> 2) + 1u];
-            tres[ln] = pack_cand(tiger_quarter(S, X, 0, prim_bases<K>(X).tiger,
-                                               Ray{V4{p4.x, p4.y, p4.z, p4.w}, V4{d4.x, d4.y, d4.z, d4.w}}, ln & 3u));
+          if constexpr (TRES_LDS) {
+            if (ln < 4u * ng) {  // quarter ln & 3 of the test of the lane ranked ln >> 2
+              const float4 p4 = tray[2u * (ln >> 2)], d4 = tray[2u * (ln >> 2) + 1u];
+              tres[ln] = pack_cand(tiger_quarter(S, X, 0, prim_bases<K>(X).tiger,
+                                                 Ray{V4{p4.x, p4.y, p4.z, p4.w}, V4{d4.x, d4.y, d4.z, d4.w}}, ln & 3u));
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (go)
+              tg = closest(closest(unpack_cand(tres[4u * rk]), unpack_cand(tres[4u * rk + 1u])),
+                           closest(unpack_cand(tres[4u * rk + 2u]), unpack_cand(tres[4u * rk + 3u])));
+          } else {
+            // the owner of rank rk pulls quarter j from lane 4 rk + j (every lane takes part in the permutes; a lane
+            // that owns no test pulls its own value and drops it)
+            float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (ln < 4u * ng) {
+              const float4 p4 = tray[2u * (ln >> 2)], d4 = tray[2u * (ln >> 2) + 1u];
+              q = pack_cand(tiger_quarter(S, X, 0, prim_bases<K>(X).tiger,
+                                          Ray{V4{p4.x, p4.y, p4.z, p4.w}, V4{d4.x, d4.y, d4.z, d4.w}}, ln & 3u));
+            }
+            auto part = [&](unsigned j) {
+              const int from = static_cast<int>(((go ? 4u * rk + j : ln) & 63u) << 2);
+              return unpack_cand(make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(q.x))),
+                                             __int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(q.y))),
+                                             __int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(q.z))), 0.0f));
+            };
+            const Cand t01 = closest(part(0u), part(1u));
+            const Cand t = closest(t01, closest(part(2u), part(3u)));
+            if (go) tg = t;
           }
-          __builtin_amdgcn_wave_barrier();
-          if (go)
-            tg = closest(closest(unpack_cand(tres[4u * rk]), unpack_cand(tres[4u * rk + 1u])),
-                         closest(unpack_cand(tres[4u * rk + 2u]), unpack_cand(tres[4u * rk + 3u])));
         }
         if (active && !parked) {
           c = need ? closest(tg, pre) : pre;
