@@ -171,12 +171,23 @@ __device__ __forceinline__ void sphere_dist2(const SphereCore2& c, float r, floa
   }
 }
 
+#ifndef RT4_SPACE_SIGN_DOT
+#define RT4_SPACE_SIGN_DOT 0  // space_cand: cos_dh = sgn * dot(norm, drct) (round 6, A/B knob)
+#endif
 __device__ __forceinline__ Cand space_cand(const rt4_scene_desc* __restrict__ S, int i, const Ray& ray) {  // :231-239
   const rt4_space& s = S->spaces[i];
   const V4 sn = ld4(s.norm);
   const float dot_vn = dot(sub(ld4(s.point), ray.point), sn);
   const float sgn = dot_vn > 0.0f ? 1.0f : (dot_vn < 0.0f ? -1.0f : 0.0f);
+#if RT4_SPACE_SIGN_DOT
+  // dot(sn * sgn, d) as sgn * dot(sn, d) (round 6, A/B knob): for sgn = +-1 the fma chain of the negated vector is the
+  // exact negation of the plain one (round-to-nearest-even is symmetric), except that an exact zero keeps +0 where the
+  // negation gives -0; for sgn = 0 both are a zero (or the same NaN class from non-finite operands). A zero is below
+  // SMALL_F either way, and a nonzero cos_dh is bit-identical, so the candidate is too: 3 VALU fewer per space.
+  const float cos_dh = sgn * dot(sn, ray.drct);
+#else
   const float cos_dh = dot(mul(sn, sgn), ray.drct);
+#endif
   Cand c{true, sgn < 0.0f, 0.0f, 0.0f, static_cast<uint32_t>(i)};
   if (cos_dh < SMALL_F) return no_cand();
   c.dist = rdiv(__builtin_fabsf(dot_vn), cos_dh);
