@@ -734,6 +734,10 @@ def main():
             if prof and cnt.get("SQ_THREAD_CYCLES_VALU"):
                 lane_ops = cnt["SQ_THREAD_CYCLES_VALU"]  # per frame (pmc_summary divides a dispatch by its frames)
                 line["roofline"]["frac_counters"] = lane_ops / (kernel_ms * 1e-3) / PEAK_VALU_LANE_OPS
+                if steady_leg:
+                    # the same frames' lane-ops over the sustained-clock leg's time: the VALU fraction once the clock
+                    # has ramped (the work per frame does not depend on the clock)
+                    steady_leg["frac_counters"] = lane_ops / (steady_leg["kernel_ms"] * 1e-3) / PEAK_VALU_LANE_OPS
                 line["roofline"]["valu_lane_ops_per_frame"] = lane_ops
                 line["roofline"]["valu_lane_utilisation"] = der.get("valu_lane_utilisation")
                 line["roofline"]["valu_issue_frac"] = der.get("valu_issue_frac")

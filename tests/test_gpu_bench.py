@@ -46,6 +46,8 @@ def test_bench_json_line():
     # the sustained-clock leg: the same frames after as many frames of load (never the value)
     st = d["steady_clock_leg"]
     assert st["intersections_per_step"] == d["intersections_per_step"] and st["frames"] >= 2 and st["value"] > 1e9
+    if rf.get("frac_counters"):
+        assert st["frac_counters"] > rf["frac_counters"] * 0.9  # the same work over a time at least as short
 
 
 def test_bench_strong_config4_one_gpu():
