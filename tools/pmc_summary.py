@@ -69,7 +69,9 @@ def main():
         # each wave64 VALU instruction needs 2 cycles of one SIMD-32
         m["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 2 / (CUS * SIMDS_PER_CU * clk * dur * 1e-9)
     if "SQ_WAVE_CYCLES" in c and "SQ_BUSY_CYCLES" in c:
-        m["avg_waves_per_simd"] = c["SQ_WAVE_CYCLES"] * 4 / (c["SQ_BUSY_CYCLES"] * 32 * SIMDS_PER_CU / 32) / 1
+        # SQ_WAVE_CYCLES counts quad-cycles per resident wave, SQ_BUSY_CYCLES cycles summed over the 32 shader engines
+        # (round 6: the earlier expression lacked both factors and read ~50 waves/SIMD)
+        m["avg_waves_per_simd"] = c["SQ_WAVE_CYCLES"] * 4 / (CUS * SIMDS_PER_CU * c["SQ_BUSY_CYCLES"] / 32)
     if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c:
         m["valu_share_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
     if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
