@@ -172,7 +172,7 @@ __device__ __forceinline__ void sphere_dist2(const SphereCore2& c, float r, floa
 }
 
 #ifndef RT4_SPACE_SIGN_DOT
-#define RT4_SPACE_SIGN_DOT 0  // space_cand: cos_dh = sgn * dot(norm, drct) (round 6, A/B knob)
+#define RT4_SPACE_SIGN_DOT 1  // space_cand: cos_dh = sgn * dot(norm, drct) (r06-v53, with RT4_BALL_BEHIND)
 #endif
 __device__ __forceinline__ Cand space_cand(const rt4_scene_desc* __restrict__ S, int i, const Ray& ray) {  // :231-239
   const rt4_space& s = S->spaces[i];
@@ -573,6 +573,21 @@ __device__ __forceinline__ void for_count(int runtime_n, F&& body) {
 
 // True when the ray's line stays clear of a bounding ball (rt4_aux.h BoundBall): the group's exact test
 // would report no hit. One 32-B scalar load, three dots.
+// RT4_BALL_BEHIND (round 6): also when the ball is behind the ray: the origin outside the inflated ball (a > R2m) and
+// the centre not ahead (b <= 0). Every forward point p + t d (t >= 0) is then at squared distance a - 2 t b + t^2 l2
+// >= a > R2m from the centre, and the exact tests report only forward hits (dist = sqrt(..) >= 0, t = s / |e| in the
+// projected plane) inside the ball (the derivation in rt4_aux.h, which R2m's 1e-3 inflation covers); the NaN-distance
+// hits of origins near a cylinder keep the exact path through the same band check. So the skip is exact too.
+#ifndef RT4_BALL_BEHIND
+#define RT4_BALL_BEHIND 1  // r06-v53 (with RT4_SPACE_SIGN_DOT): config 5 +1.5 % on two boxes (profiles/r06_ab.txt)
+#endif
+// BEHIND: the kernel's shape takes the second test (RT4_BALL_BEHIND; not in the closed rooms' kernels, >= 3 spaces,
+// where it spilled in the loop at their wave bound)
+template <uint32_t SH>
+constexpr bool ball_behind_of() {
+  return RT4_BALL_BEHIND != 0 && (RT4_BALL_BEHIND == 2 || ((SH >> 8) & 0xFFu) < 4);
+}
+template <bool BEHIND = false>
 __device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray) {
   const f16v k = *reinterpret_cast<const f16v*>(&bb);  // centre, a1, a2, r2m, band[0..2]
   const f16v m = *(reinterpret_cast<const f16v*>(&bb) + 1);  // band[3..7]
@@ -582,7 +597,8 @@ __device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray) {
   const float dB = fmaf_(u1, u1, u2 * u2), dA = a - dB;  // squared distances to plane B and plane A
   const bool near_surface = (dA >= k[13] && dA <= k[14]) || (dA >= k[15] && dA <= m[0]) ||
                             (dB >= m[1] && dB <= m[2]) || (dB >= m[3] && dB <= m[4]);
-  return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && (a - fmaf_(4e-6f, a, k[12])) * l2 > b * b;
+  const bool behind = BEHIND && b <= 0.0f && a > k[12];
+  return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && ((a - fmaf_(4e-6f, a, k[12])) * l2 > b * b || behind);
 }
 
 // Flat primitive-table index of each group's first entry (rt4_aux.h SceneAux::prims order): compile-time
@@ -712,10 +728,10 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
 #endif
     });
   if (K & K_UNION)
-    if (!(RT4_BOUND_SKIP && far_from(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
+    if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>()>(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
   if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && (RT4_HYPER_AXIS_TIGER || !(K & K_TIGER))>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
   if ((K & K_TIGER) && WITH_TIGER)
-    if (!(RT4_BOUND_SKIP && far_from(X->tiger_bound[0], ray))) {
+    if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>()>(X->tiger_bound[0], ray))) {
 #ifdef RT4_LANESTATS  // diagnostic: tiger tests and their active lanes (counter[60], [61])
       {
         const unsigned long long ex = __builtin_amdgcn_read_exec();
