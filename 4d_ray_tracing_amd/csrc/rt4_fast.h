@@ -587,8 +587,9 @@ template <uint32_t SH>
 constexpr bool ball_behind_of() {
   return RT4_BALL_BEHIND != 0 && (RT4_BALL_BEHIND == 2 || ((SH >> 8) & 0xFFu) < 4);
 }
-template <bool BEHIND = false>
-__device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray) {
+// LINE = false: only the occlusion test (the hypercube's ball: its parallel faces' +inf hits forbid the line skip)
+template <bool BEHIND = false, bool OCC = false, bool LINE = true>
+__device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray, const Cand* acc = nullptr) {
   const f16v k = *reinterpret_cast<const f16v*>(&bb);  // centre, a1, a2, r2m, band[0..2]
   const f16v m = *(reinterpret_cast<const f16v*>(&bb) + 1);  // band[3..7]
   const V4 pc = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
@@ -598,9 +599,32 @@ __device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray) {
   const bool near_surface = (dA >= k[13] && dA <= k[14]) || (dA >= k[15] && dA <= m[0]) ||
                             (dB >= m[1] && dB <= m[2]) || (dB >= m[3] && dB <= m[4]);
   const bool behind = BEHIND && b <= 0.0f && a > k[12];
-  return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && ((a - fmaf_(4e-6f, a, k[12])) * l2 > b * b || behind);
+  if constexpr (!OCC && LINE)  // r06-v53's expression as it was (the same code in the kernels without the knob)
+    return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && ((a - fmaf_(4e-6f, a, k[12])) * l2 > b * b || behind);
+  const bool in_range = a < 1e30f && l2 > 1e-30f && l2 < 1e30f;
+  bool occ = false;
+  if constexpr (OCC) {  // RT4_OCCLUDE_SKIP (below): the ball starts beyond acc's hit
+    const float x = b - acc->dist * l2 - 5e-5f * (a + l2);
+    occ = acc->hit && x > 0.0f && x * x > k[12] * l2;
+  }
+  return in_range && ((LINE && !near_surface && ((a - fmaf_(4e-6f, a, k[12])) * l2 > b * b || behind)) || occ);
 }
 
+// Occlusion skip (round 6, RT4_OCCLUDE_SKIP: 1 = tiger and union, 3 = also the hypercube): a group whose bounding ball
+// starts beyond the closest hit so far cannot change it. Every hit the group's exact test reports lies in the inflated
+// ball (rt4_aux.h BoundBall; the hypercube's finite hits lie on its cells' faces, inside hyper_bound), so its distance
+// t satisfies t l2 >= b - sqrt(R2m l2) (b = (c - p).d, l2 = |d|^2), and closest() keeps acc for any t >= acc.dist
+// (ties keep acc; NaN and +inf distances never replace a hit). The test skips when
+//   x = b - acc.dist l2 - 5e-5 (a + l2) > 0  and  x^2 > R2m l2,
+// where 5e-5 (a + l2) >= 1e-4 sqrt(a l2) covers the fp32 rounding of b, of the products and of the hit point itself
+// (each ~1e-6 sqrt(a l2)). acc without a hit, or with a NaN or infinite distance, never skips.
+#ifndef RT4_OCCLUDE_SKIP
+#define RT4_OCCLUDE_SKIP 0
+#endif
+template <uint32_t SH>
+constexpr bool occlude_of(int what) {  // what: 1 = tiger / union, 2 = hypercube; not in the closed rooms' kernels
+  return (RT4_OCCLUDE_SKIP & what) != 0 && ((SH >> 8) & 0xFFu) < 4;
+}
 // Flat primitive-table index of each group's first entry (rt4_aux.h SceneAux::prims order): compile-time
 // for exact-count shapes (the scene-shape check pins one union / hypercube / tiger), else read.
 struct PrimBases {
@@ -728,10 +752,13 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
 #endif
     });
   if (K & K_UNION)
-    if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>()>(X->union_bound[0], ray))) inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
-  if (K & K_HYPERCUBE) inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && (RT4_HYPER_AXIS_TIGER || !(K & K_TIGER))>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
+    if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>(), occlude_of<SH>(1)>(X->union_bound[0], ray, &inter)))
+      inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
+  if (K & K_HYPERCUBE)
+    if (!(occlude_of<SH>(2) && far_from<false, true, false>(X->hyper_bound[0], ray, &inter)))
+      inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && (RT4_HYPER_AXIS_TIGER || !(K & K_TIGER))>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
   if ((K & K_TIGER) && WITH_TIGER)
-    if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>()>(X->tiger_bound[0], ray))) {
+    if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>(), occlude_of<SH>(1)>(X->tiger_bound[0], ray, &inter))) {
 #ifdef RT4_LANESTATS  // diagnostic: tiger tests and their active lanes (counter[60], [61])
       {
         const unsigned long long ex = __builtin_amdgcn_read_exec();

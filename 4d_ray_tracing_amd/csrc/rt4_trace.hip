@@ -1094,7 +1094,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
           fresh = true;
         } else {
           pre = find_cand<K, false>(S, X, P, ray);  // every group but the tiger, in order
-          need = !(RT4_BOUND_SKIP && far_from<ball_behind_of<K>()>(X->tiger_bound[0], ray));
+          need = !(RT4_BOUND_SKIP && far_from<ball_behind_of<K>(), occlude_of<K>(1)>(X->tiger_bound[0], ray, &pre));
         }
       }
       if constexpr (SDEFER) {
@@ -1117,7 +1117,7 @@ __global__ __launch_bounds__(256, min_waves_of(K, REUSE, LUT)) void rt4_trace_ke
         }
         if (fresh) {
           pre = find_rest<K, false>(S, X, P, ray, exact_pending<K, false>(X, P, ray, geo, pend, inter));
-          need = !(RT4_BOUND_SKIP && far_from<ball_behind_of<K>()>(X->tiger_bound[0], ray));
+          need = !(RT4_BOUND_SKIP && far_from<ball_behind_of<K>(), occlude_of<K>(1)>(X->tiger_bound[0], ray, &pre));
         }
       }
       if constexpr (TSERVE) {
