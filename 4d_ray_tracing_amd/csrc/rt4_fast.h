@@ -578,8 +578,11 @@ __device__ __forceinline__ void for_count(int runtime_n, F&& body) {
 // >= a > R2m from the centre, and the exact tests report only forward hits (dist = sqrt(..) >= 0, t = s / |e| in the
 // projected plane) inside the ball (the derivation in rt4_aux.h, which R2m's 1e-3 inflation covers); the NaN-distance
 // hits of origins near a cylinder keep the exact path through the same band check. So the skip is exact too.
+#ifndef RT4_BALL_BEHIND_MAX
+#define RT4_BALL_BEHIND_MAX 1  // r06-v54: the behind test as max(b, 0) inside the line test (fits the mirror room's registers)
+#endif
 #ifndef RT4_BALL_BEHIND
-#define RT4_BALL_BEHIND 1  // r06-v53 (with RT4_SPACE_SIGN_DOT): config 5 +1.5 % on two boxes (profiles/r06_ab.txt)
+#define RT4_BALL_BEHIND 2  // r06-v53: 1 (not the closed rooms; config 5 +1.5 %); r06-v54: 2, every kernel (config 4 +3.1 %)
 #endif
 // BEHIND: the kernel's shape takes the second test (RT4_BALL_BEHIND; not in the closed rooms' kernels, >= 3 spaces,
 // where it spilled in the loop at their wave bound)
@@ -598,6 +601,14 @@ __device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray, co
   const float dB = fmaf_(u1, u1, u2 * u2), dA = a - dB;  // squared distances to plane B and plane A
   const bool near_surface = (dA >= k[13] && dA <= k[14]) || (dA >= k[15] && dA <= m[0]) ||
                             (dB >= m[1] && dB <= m[2]) || (dB >= m[3] && dB <= m[4]);
+#if RT4_BALL_BEHIND_MAX
+  // the same skip as one v_max: with b clamped at 0 the line test reads a (1 - 4e-6) > R2m when b <= 0, i.e. the origin
+  // outside the inflated ball (a finite b: a, l2 < 1e30)
+  if constexpr (BEHIND && !OCC && LINE) {
+    const float bp = fmaxf(b, 0.0f);
+    return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && (a - fmaf_(4e-6f, a, k[12])) * l2 > bp * bp;
+  }
+#endif
   const bool behind = BEHIND && b <= 0.0f && a > k[12];
   if constexpr (!OCC && LINE)  // r06-v53's expression as it was (the same code in the kernels without the knob)
     return !near_surface && a < 1e30f && l2 > 1e-30f && l2 < 1e30f && ((a - fmaf_(4e-6f, a, k[12])) * l2 > b * b || behind);

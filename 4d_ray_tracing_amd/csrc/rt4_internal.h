@@ -11,7 +11,7 @@
 // Version of the trace kernel (the third word of rt4_build_info): bench.py records it and takes
 // roofline.traffic only from a rocprofv3 profile of the same version (profiles/). Bump on every
 // change to the device code.
-#define RT4_KERNEL_VERSION "r06-v53"
+#define RT4_KERNEL_VERSION "r06-v54"
 
 // Writes a formatted message into err (if non-NULL); returns 0 so it composes in expressions.
 inline int rt4_set_err(char* err, size_t errlen, const char* fmt, ...) {
