@@ -621,6 +621,22 @@ __device__ __forceinline__ bool far_from(const BoundBall& bb, const Ray& ray, co
   return in_range && ((LINE && !near_surface && ((a - fmaf_(4e-6f, a, k[12])) * l2 > b * b || behind)) || occ);
 }
 
+// Hypercube skip behind a hit (round 6, RT4_HYPER_SKIP, A/B knob): the hypercube's finite hits lie on its cells, inside
+// hyper_bound's inflated ball; its +inf (parallel face) and NaN hits never replace a hit with a finite distance. So when
+// acc already holds such a hit and the ray's line clears the ball, or the ball is behind the ray (the max(b, 0) form),
+// the hypercube cannot change acc and its test is skipped.
+#ifndef RT4_HYPER_SKIP
+#define RT4_HYPER_SKIP 0
+#endif
+__device__ __forceinline__ bool hyper_skip(const BoundBall& bb, const Ray& ray, const Cand& acc) {
+  const f16v k = *reinterpret_cast<const f16v*>(&bb);
+  const V4 pc = sub(V4{k[0], k[1], k[2], k[3]}, ray.point);
+  const float a = dot(pc, pc), b = dot(pc, ray.drct), l2 = dot(ray.drct, ray.drct);
+  const float bp = fmaxf(b, 0.0f);
+  return acc.hit && acc.dist < 3.0e38f && a < 1e30f && l2 > 1e-30f && l2 < 1e30f &&
+         (a - fmaf_(4e-6f, a, k[12])) * l2 > bp * bp;
+}
+
 // Occlusion skip (round 6, RT4_OCCLUDE_SKIP: 1 = tiger and union, 3 = also the hypercube): a group whose bounding ball
 // starts beyond the closest hit so far cannot change it. Every hit the group's exact test reports lies in the inflated
 // ball (rt4_aux.h BoundBall; the hypercube's finite hits lie on its cells' faces, inside hyper_bound), so its distance
@@ -766,7 +782,8 @@ __device__ __forceinline__ Cand find_rest(const rt4_scene_desc* __restrict__ S, 
     if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>(), occlude_of<SH>(1)>(X->union_bound[0], ray, &inter)))
       inter = closest(union_cand(S, X, 0, B.uni, ray), inter);
   if (K & K_HYPERCUBE)
-    if (!(occlude_of<SH>(2) && far_from<false, true, false>(X->hyper_bound[0], ray, &inter)))
+    if (!(occlude_of<SH>(2) && far_from<false, true, false>(X->hyper_bound[0], ray, &inter)) &&
+        !(RT4_HYPER_SKIP && hyper_skip(X->hyper_bound[0], ray, inter)))
       inter = closest(hypercube_cand<RT4_HYPER_PENDING != 0, RT4_HYPER_AXIS && (RT4_HYPER_AXIS_TIGER || !(K & K_TIGER))>(S, X, reinterpret_cast<const float4*>(P) - HYPER_CELLS_LDS, 0, B.cube, ray), inter);
   if ((K & K_TIGER) && WITH_TIGER)
     if (!(RT4_BOUND_SKIP && far_from<ball_behind_of<SH>(), occlude_of<SH>(1)>(X->tiger_bound[0], ray, &inter))) {
