@@ -682,6 +682,9 @@ __device__ __forceinline__ PrimBases prim_bases(const SceneAux* __restrict__ X) 
 #ifndef RT4_SPHERE_GEO
 #define RT4_SPHERE_GEO 1
 #endif
+#ifndef RT4_CULL_MAX
+#define RT4_CULL_MAX 0
+#endif
 constexpr int GEO_MAX = 2;
 template <uint32_t SH>
 constexpr int geo_spheres() {
@@ -720,7 +723,19 @@ __device__ __forceinline__ Cand find_pre(const rt4_scene_desc* __restrict__ S, c
 #ifdef RT4_CULL_BITWISE  // A/B build only: the same predicate without short-circuit branches
       const bool skip = outside & ((dp < 0.0f) | (d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5])));
 #else
-      const bool skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5]));
+      bool skip;
+      if constexpr (RT4_CULL_MAX && !(K & K_TIGER)) {
+        // round 6 (A/B knob; not next to a tiger, where it spilled): dp clamped at 0 folds the "outside and pointing
+        // away" early-out into the one test: for dp < 0 it reads d2 > fma(K, d2, r2m) > r^2 (1 + 1e-4), so len_po >= r
+        // and the exact path's own early-out (:205) returns no hit; outside rays nearer the surface than that now run
+        // the exact path, which returns the same no hit; inside rays are never culled (d2 < r^2 < the threshold); a NaN
+        // dp stays NaN (a select, not max), so such rays are not culled, as before.
+        (void)outside;
+        const float bp = dp < 0.0f ? 0.0f : dp;
+        skip = d2 - bp * bp > fmaf_(SPHERE_CULL_K, d2, k[5]);
+      } else {
+        skip = outside && (dp < 0.0f || d2 - dp * dp > fmaf_(SPHERE_CULL_K, d2, k[5]));
+      }
 #endif
       pend |= skip ? 0u : (1u << i);
     });
